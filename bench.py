@@ -1,0 +1,274 @@
+#!/usr/bin/env python3
+"""Headline benchmark: 64-bit coefficients/s for c = INTT(NTT(a) (.) b) on
+N = 2^16, 16 towers, batch 1024 per GPU (BASELINE.json configs[2]), with the
+dominant kernel's HBM-roofline fraction and a CPU baseline on the host cores.
+
+Single GPU:   python bench.py [--steps K --warmup W]
+N GPUs:       python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 \
+                  --master-port P bench.py --gpus N
+Each rank processes its own batch shard (weak scaling: per-GPU work fixed, no
+collective on the data path).  RCCL is used once at setup to broadcast a
+synthetic evaluation key from rank 0 (the only exchange the north star names).
+
+Prints ONE JSON line on rank 0.
+"""
+import argparse
+import json
+import os
+import socket
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "upmem--openfhe_amd"))
+
+METRIC = "64-bit coeffs/sec for NTT+Hadamard+INTT, N=2^16, 16 towers; % HBM roofline"
+HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8 TB/s spec
+ALG_BYTES_PER_COEFF = 24       # read a, read b, write c
+STAGE_NAMES = {0: "k_cols<fwd>", 1: "k_block<fused>", 2: "k_cols<inv>"}
+
+
+def moduli_chain(log_n, towers, bits=60):
+    """poly-benchmark modulus chain (benchmark/src/poly-benchmark-16k.cpp:89-96)
+    and minimal primitive 2N-th roots (nbtheory-impl.h:183-231).  Product-side
+    setup code (not the oracle): deterministic Miller-Rabin in Python ints."""
+    m = 2 << log_n
+
+    def is_prime(n):
+        if n < 2:
+            return False
+        for p in (2, 3, 5, 7, 11, 13, 17, 19, 23, 29, 31, 37):
+            if n % p == 0:
+                return n == p
+        d, s = n - 1, 0
+        while d % 2 == 0:
+            d //= 2
+            s += 1
+        for a in (2, 3, 5, 7, 11, 13, 17, 19, 23, 29, 31, 37):
+            x = pow(a, d, n)
+            if x in (1, n - 1):
+                continue
+            for _ in range(s - 1):
+                x = x * x % n
+                if x == n - 1:
+                    break
+            else:
+                return False
+        return True
+
+    q = (1 << bits) + 1
+    while not is_prime(q):
+        q += m
+    qs, roots = [], []
+    for _ in range(towers):
+        q -= m
+        while not is_prime(q):
+            q -= m
+        qs.append(q)
+        e = (q - 1) // m
+        c = 2
+        while True:
+            x = pow(c, e, q)
+            if pow(x, m // 2, q) == q - 1:
+                break
+            c += 1
+        x2 = x * x % q
+        best, y = x, x
+        for _ in range(m // 2 - 1):
+            y = y * x2 % q
+            if y < best:
+                best = y
+        roots.append(best)
+    return qs, roots
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--log-n", type=int, default=16)
+    ap.add_argument("--towers", type=int, default=16)
+    ap.add_argument("--batch", type=int, default=1024, help="polynomials per GPU")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget (0 = skip)")
+    ap.add_argument("--no-check", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    import ofhe_hip as H
+
+    ctx = H.Context(local)
+    log_n, T, B = args.log_n, args.towers, args.batch
+    n = 1 << log_n
+    qs, roots = moduli_chain(log_n, T)
+    plan = H.NTTPlan(ctx, log_n, qs, roots)
+
+    # synthetic inputs, uniform residues mod q_t, generated on the device
+    g = torch.Generator(device=dev)
+    g.manual_seed(0x5EED + rank)
+    a = torch.empty((B, T, n), dtype=torch.int64, device=dev)
+    b = torch.empty((B, T, n), dtype=torch.int64, device=dev)
+    for t, q in enumerate(qs):
+        a[:, t, :].random_(0, q, generator=g)
+        b[:, t, :].random_(0, q, generator=g)
+    c = torch.empty_like(a)
+    stream = torch.cuda.current_stream(dev)
+    sp = stream.cuda_stream
+
+    # RCCL broadcast of a synthetic evaluation key (setup, outside the timed loop)
+    bcast = None
+    if world > 1:
+        dnum = 3
+        key = torch.empty((2 * dnum, T + (T + dnum - 1) // dnum, n), dtype=torch.int64, device=dev)
+        if rank == 0:
+            key.random_(0, qs[-1], generator=g)
+        dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        dist.broadcast(key, src=0)
+        torch.cuda.synchronize()
+        bcast = {"bytes": key.numel() * 8, "ms": (time.perf_counter() - t0) * 1e3, "backend": "nccl(RCCL)"}
+        del key
+
+    def step():
+        plan.ntt_mul_intt(a.data_ptr(), b.data_ptr(), c.data_ptr(), B, sp)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        e = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(e, op=dist.ReduceOp.MAX)
+        elapsed = float(e.item())
+    coeffs_per_step = B * T * n * world
+    value = coeffs_per_step * args.steps / elapsed
+    ms_per_step = elapsed / args.steps * 1e3
+
+    # per-kernel durations with HIP events on the launch stream (separate pass)
+    kernels = {}
+    reps = max(3, min(args.steps, 10))
+    for st in (0, 1, 2):
+        if log_n <= 12 and st != 1:
+            continue
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        plan.ntt_mul_intt_stage(0, a.data_ptr(), b.data_ptr(), c.data_ptr(), B, sp)
+        plan.ntt_mul_intt_stage(1, a.data_ptr(), b.data_ptr(), c.data_ptr(), B, sp)
+        ev0.record(stream)
+        for _ in range(reps):
+            plan.ntt_mul_intt_stage(st, a.data_ptr(), b.data_ptr(), c.data_ptr(), B, sp)
+        ev1.record(stream)
+        ev1.synchronize()
+        kernels[STAGE_NAMES[st]] = ev0.elapsed_time(ev1) / reps
+    dominant = max(kernels, key=kernels.get)
+    kms = kernels[dominant]
+    coeffs_rank = B * T * n
+    achieved = ALG_BYTES_PER_COEFF * coeffs_rank / (kms * 1e-3) / 1e9
+    traffic = None
+    pmc_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if os.path.exists(pmc_path):
+        try:
+            pm = json.load(open(pmc_path))
+            ent = pm.get("kernels", {}).get(dominant)
+            if ent and ent.get("batch") == B and ent.get("log_n") == log_n and ent.get("towers") == T:
+                traffic = ent.get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+
+    # spot parity check against the oracle (one tower of two batch entries)
+    parity = None
+    if not args.no_check and rank == 0:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import numpy as np
+        import oracle as O
+
+        step()
+        torch.cuda.synchronize()
+        ok = True
+        for bi, ti in ((0, 0), (B - 1, T - 1)):
+            tb = O.Tables(n, [qs[ti]], [roots[ti]])
+            aa = a[bi, ti].cpu().numpy().view(np.uint64).reshape(1, 1, n)
+            bb = b[bi, ti].cpu().numpy().view(np.uint64).reshape(1, 1, n)
+            cc = c[bi, ti].cpu().numpy().view(np.uint64).reshape(1, 1, n)
+            ok = ok and bool(np.array_equal(cc, O.ntt_mul_intt(aa, bb, tb)))
+        parity = ok
+
+    # CPU baseline: the oracle (C, OpenMP over batch x towers) on a bounded sample
+    cpu = None
+    if rank == 0 and world == 1 and args.cpu_seconds > 0:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import numpy as np
+        import oracle as O
+
+        Bs = 4
+        tbs = O.Tables(n, qs, roots)
+        ca = O.uniform_dcrt(Bs, T, n, qs, 1)
+        cb = O.uniform_dcrt(Bs, T, n, qs, 2)
+        O.ntt_mul_intt(ca, cb, tbs)  # warm
+        runs, t0 = 0, time.perf_counter()
+        while True:
+            O.ntt_mul_intt(ca, cb, tbs)
+            runs += 1
+            el = time.perf_counter() - t0
+            if el >= args.cpu_seconds:
+                break
+        cpu = {"value": runs * Bs * T * n / el, "unit": "coeffs/s", "cores": int(O.lib().oracle_num_threads()),
+               "kind": "port",
+               "sample": f"{runs} runs x {Bs} polys x {T} towers x N=2^{log_n} ({el:.1f} s), "
+                         f"oracle/ofhe_oracle.c OpenMP over batch x towers, host {socket.gethostname()}"}
+
+    if rank == 0:
+        out = {
+            "metric": METRIC,
+            "value": value,
+            "unit": "coeffs/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": ms_per_step,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u64",
+            "data": "synthetic: uniform residues mod q_t (torch random_ on device), a coeff form, b eval form",
+            "config": {"workload": f"configs[2]: N=2^{log_n}, towers={T}, batch={B} per GPU, "
+                                   "c = INTT(NTT(a) (.) b)",
+                       "log_n": log_n, "towers": T, "batch_per_gpu": B, "global_batch": B * world,
+                       "parallelism": f"batch-sharded x{world} (no data-path collective)"},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": dominant,
+                         "kernel_ms": kms, "alg_bytes_per_launch": ALG_BYTES_PER_COEFF * coeffs_rank},
+            "pipeline_hbm_frac": value / world * ALG_BYTES_PER_COEFF / (HBM_PEAK_GBS * 1e9),
+            "kernels_ms": kernels,
+            "cpu_baseline": cpu,
+            "parity_spot_check": parity,
+            "evalkey_broadcast": bcast,
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,142 @@
+/*
+ * ofhe_hip.h -- C ABI of the MI355X (gfx950) RNS polynomial backend.
+ *
+ * This is the drop-in boundary that replaces the UPMEM interception layer of
+ * MpokiAbel/UPMEM--OpenFHE (src/core/include/pim/PimManager.h,
+ * src/core/include/pim/PimData.h, src/core/pim/host/PimManager.cpp) and the
+ * CPU hot loops it was meant to offload:
+ *   - ChineseRemainderTransformFTTNat forward / inverse NTT
+ *       (src/core/include/math/hal/intnat/transformnat-impl.h:575-705),
+ *   - NativeVectorT element-wise ModMul/ModAdd/ModSub
+ *       (src/core/include/math/hal/intnat/mubintvecnat.h:426-432,501-513;
+ *        src/core/lib/math/hal/intnat/mubintvecnat.cpp:245-367),
+ *   - DCRTPolyImpl::ApproxSwitchCRTBasis
+ *       (src/core/include/lattice/hal/default/dcrtpoly-impl.h:1034-1063).
+ *
+ * Conventions
+ *   - Plain C, no exceptions cross the ABI. Every entry point returns an int
+ *     status (OFHE_OK = 0); ofhe_hip_last_error() gives a thread-local message.
+ *     The C++ adapter (upmem--openfhe_amd/host/ofhe_dcrt.hpp) turns non-zero
+ *     into lbcrypto-style math_error exceptions, as OPENFHE_THROW does.
+ *   - Polynomial data is uint64_t residues laid out [batch][tower][N],
+ *     contiguous, in DEVICE memory, unless a function says otherwise.
+ *     Inputs must be canonical residues in [0, q_t); outputs are canonical.
+ *   - `stream` is a hipStream_t passed as void* (NULL = default stream).
+ *     Calls are asynchronous on that stream; nothing here synchronises.
+ *   - The caller owns all data buffers; the library owns contexts, plans,
+ *     twiddle tables and scratch.
+ */
+#ifndef OFHE_HIP_H
+#define OFHE_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum {
+    OFHE_OK = 0,
+    OFHE_ERR_ARG = 1,     /* invalid argument (size, modulus, root ...)     */
+    OFHE_ERR_HIP = 2,     /* a HIP runtime call failed                       */
+    OFHE_ERR_NOMEM = 3,   /* device or host allocation failed                */
+    OFHE_ERR_STATE = 4    /* use of a destroyed / uninitialised object       */
+};
+
+typedef struct ofhe_ctx_s* ofhe_ctx_t;   /* one per device (PimManager::getPim) */
+typedef struct ofhe_plan_s* ofhe_plan_t; /* NTT plan: (N, towers, q[], psi[])  */
+
+/* Thread-local description of the last failure in this thread. */
+const char* ofhe_hip_last_error(void);
+
+/* Library version string ("ofhe-hip <ver> gfx950"). */
+const char* ofhe_hip_version(void);
+
+/* ---- device context: replaces PimManager::getPim(nr_dpus, profile),
+ *      PimManager.h:23-29 (lazily created singleton), and its allocator /
+ *      transfers (PimManager.cpp:5-93). --------------------------------- */
+int ofhe_hip_device_count(int* count);
+int ofhe_hip_init(int device, ofhe_ctx_t* ctx);
+int ofhe_hip_finalize(ofhe_ctx_t ctx);
+/* PimManager::allocate / deallocate (PimManager.h:83-85) */
+int ofhe_hip_alloc(ofhe_ctx_t ctx, size_t bytes, void** dptr);
+int ofhe_hip_free(ofhe_ctx_t ctx, void* dptr);
+/* PimManager::copy_to_pim (scatter, type 0) / copy_from_pim (PimManager.h:44-54) */
+int ofhe_hip_copy_to_device(ofhe_ctx_t ctx, void* dst, const void* src, size_t bytes, void* stream);
+int ofhe_hip_copy_to_host(ofhe_ctx_t ctx, void* dst, const void* src, size_t bytes, void* stream);
+/* device-to-device copy (poly copy constructor, poly.h:368 owns its vector) */
+int ofhe_hip_copy_device(ofhe_ctx_t ctx, void* dst, const void* src, size_t bytes, void* stream);
+/* PimManager::start_kernel is synchronous (PimManager.h:68); here explicit. */
+int ofhe_hip_sync(ofhe_ctx_t ctx, void* stream);
+
+/* ---- NTT plan: replaces ChineseRemainderTransformFTTNat::PreCompute and
+ *      its static twiddle maps (transformnat-impl.h:708-763,
+ *      transformnat.h:352-368).  N = 2^log_n, 1 <= log_n <= 17; q[t] prime,
+ *      q[t] = 1 mod 2N, q[t] < 2^60; psi[t] a primitive 2N-th root of unity
+ *      mod q[t] (OpenFHE uses the smallest one, nbtheory-impl.h:183-231).
+ *      Tables are built on the host once and kept resident on the device. */
+int ofhe_hip_plan_create(ofhe_ctx_t ctx, uint32_t log_n, uint32_t towers, const uint64_t* q,
+                         const uint64_t* psi, ofhe_plan_t* plan);
+int ofhe_hip_plan_destroy(ofhe_plan_t plan);
+/* Copy the plan's host-side tables out (debug / parity tests): any pointer
+ * may be NULL.  tab*: [towers][N] in OpenFHE order (Table[rev(i)] = psi^i). */
+int ofhe_hip_plan_tables(ofhe_plan_t plan, uint64_t* tab, uint64_t* tab_pre, uint64_t* itab,
+                         uint64_t* itab_pre, uint64_t* ninv);
+
+/* Forward negacyclic NTT in place, natural order -> bit-reversed evaluation
+ * order: ChineseRemainderTransformFTT<NativeVector>::ForwardTransformToBitReverseInPlace
+ * (transformnat-impl.h:575-602 -> 300-354), for every (batch, tower). */
+int ofhe_hip_ntt_fwd(ofhe_plan_t plan, uint64_t* data, uint32_t batch, void* stream);
+/* Inverse NTT in place, bit-reversed -> natural, n^-1 applied:
+ * InverseTransformFromBitReverseInPlace (transformnat-impl.h:637-666 -> 492-552). */
+int ofhe_hip_ntt_inv(ofhe_plan_t plan, uint64_t* data, uint32_t batch, void* stream);
+
+/* c = a (op) b element-wise per tower: NativeVectorT::ModMul (Barrett,
+ * mubintvecnat.cpp:353-367 / .h:501-513), ModAdd (.cpp:245-264 / .h:426-432),
+ * ModSub (.cpp:301-307).  c may alias a or b (the *Eq forms). */
+int ofhe_hip_modmul_vv(ofhe_plan_t plan, const uint64_t* a, const uint64_t* b, uint64_t* c,
+                       uint32_t batch, void* stream);
+int ofhe_hip_modadd_vv(ofhe_plan_t plan, const uint64_t* a, const uint64_t* b, uint64_t* c,
+                       uint32_t batch, void* stream);
+int ofhe_hip_modsub_vv(ofhe_plan_t plan, const uint64_t* a, const uint64_t* b, uint64_t* c,
+                       uint32_t batch, void* stream);
+/* c = a * s[t] mod q[t] with one scalar per tower (host array [towers]):
+ * NativeVectorT::ModMul(const IntegerType&) (mubintvecnat.cpp:310-332, Shoup). */
+int ofhe_hip_modmul_scalar(ofhe_plan_t plan, const uint64_t* a, const uint64_t* s, uint64_t* c,
+                           uint32_t batch, void* stream);
+
+/* The metric pipeline, per (batch, tower): c = INTT(NTT(a) (.) b), a in
+ * coefficient form, b in evaluation form, c in coefficient form.  Equals
+ * SwitchFormat -> Times -> SwitchFormat on DCRTPoly (dcrtpoly-impl.h:2518-2524,
+ * dcrtpoly.h:185-200).  c may alias a. */
+int ofhe_hip_ntt_mul_intt(ofhe_plan_t plan, const uint64_t* a, const uint64_t* b, uint64_t* c,
+                          uint32_t batch, void* stream);
+
+/* One launch of the pipeline above, for per-kernel timing (bench.py):
+ * stage 0 = forward column pass (a -> c), 1 = block pass (forward tail,
+ * Hadamard with b, inverse head; reads c, or a when log_n <= 12),
+ * 2 = inverse column pass (c -> c).  Stages 0 and 2 are no-ops for
+ * log_n <= 12.  Running 0, 1, 2 in order equals ofhe_hip_ntt_mul_intt. */
+int ofhe_hip_ntt_mul_intt_stage(ofhe_plan_t plan, int stage, const uint64_t* a, const uint64_t* b,
+                                uint64_t* c, uint32_t batch, void* stream);
+
+/* ---- RNS base conversion: DCRTPolyImpl::ApproxSwitchCRTBasis
+ *      (dcrtpoly-impl.h:1034-1063, Mul128/BarrettUint128ModUint64 in
+ *      utils/utilities-int.h:47-103).  x: [batch][size_q][N] coefficient form
+ *      mod q[i]; out: [batch][size_p][N] mod p[j].  Precomputations as the pke
+ *      layer builds them (pke/lib/schemerns/rns-cryptoparameters.cpp:273-337):
+ *      qhat_inv_modq[i] = (Q/q_i)^-1 mod q_i, qhat_modp[i*size_p+j] = (Q/q_i) mod p_j,
+ *      all host arrays.  Barrett constants are derived internally. */
+typedef struct ofhe_bconv_s* ofhe_bconv_t;
+int ofhe_hip_bconv_create(ofhe_ctx_t ctx, uint32_t log_n, uint32_t size_q, uint32_t size_p,
+                          const uint64_t* q, const uint64_t* p, const uint64_t* qhat_inv_modq,
+                          const uint64_t* qhat_modp, ofhe_bconv_t* bconv);
+int ofhe_hip_bconv_destroy(ofhe_bconv_t bconv);
+int ofhe_hip_approx_switch_crt_basis(ofhe_bconv_t bconv, const uint64_t* x, uint64_t* out,
+                                     uint32_t batch, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* OFHE_HIP_H */

@@ -1,0 +1,240 @@
+// C++ parity tests through the host adapter (upmem--openfhe_amd/host/ofhe_dcrt.hpp)
+// and the C ABI, written like the reference's own gtest suites (gtest is an
+// empty submodule in the reference, so this is a minimal self-contained runner).
+#include <cstdio>
+#include <cstdlib>
+#include <functional>
+#include <random>
+#include <string>
+#include <vector>
+
+#include "../../upmem--openfhe_amd/host/ofhe_dcrt.hpp"
+
+using namespace ofhe;
+typedef unsigned __int128 u128;
+
+static int g_fail = 0, g_run = 0;
+#define EXPECT_EQ(a, b, msg)                                                                 \
+    do {                                                                                     \
+        if (!((a) == (b))) {                                                                 \
+            std::printf("  FAIL %s:%d %s\n", __FILE__, __LINE__, std::string(msg).c_str()); \
+            g_fail++;                                                                        \
+        }                                                                                    \
+    } while (0)
+#define EXPECT_THROW(stmt, ex, msg)                                                               \
+    do {                                                                                          \
+        bool thrown_ = false;                                                                     \
+        try {                                                                                     \
+            stmt;                                                                                 \
+        } catch (const ex&) {                                                                     \
+            thrown_ = true;                                                                       \
+        }                                                                                         \
+        if (!thrown_) {                                                                           \
+            std::printf("  FAIL %s:%d expected " #ex " %s\n", __FILE__, __LINE__, std::string(msg).c_str()); \
+            g_fail++;                                                                             \
+        }                                                                                         \
+    } while (0)
+
+// --- small host number theory for test parameters (nbtheory-impl.h semantics) ---
+static uint64_t mulmod(uint64_t a, uint64_t b, uint64_t q) { return (uint64_t)((u128)a * b % q); }
+static uint64_t powmod(uint64_t b, uint64_t e, uint64_t q) {
+    uint64_t r = 1 % q;
+    for (b %= q; e; e >>= 1, b = mulmod(b, b, q))
+        if (e & 1) r = mulmod(r, b, q);
+    return r;
+}
+static bool is_prime(uint64_t n) {
+    if (n < 2) return false;
+    for (uint64_t p : {2, 3, 5, 7, 11, 13, 17, 19, 23, 29, 31, 37})
+        if (n % p == 0) return n == p;
+    uint64_t d = n - 1;
+    int s = 0;
+    while (!(d & 1)) d >>= 1, s++;
+    for (uint64_t a : {2, 3, 5, 7, 11, 13, 17, 19, 23, 29, 31, 37}) {
+        uint64_t x = powmod(a, d, n);
+        if (x == 1 || x == n - 1) continue;
+        bool comp = true;
+        for (int r = 1; r < s && comp; r++) {
+            x = mulmod(x, x, n);
+            if (x == n - 1) comp = false;
+        }
+        if (comp) return false;
+    }
+    return true;
+}
+static uint64_t first_prime(unsigned bits, uint64_t m) {  // FirstPrime
+    uint64_t q = (1ull << bits) + 1;
+    if ((1ull << bits) % m) q += m - (1ull << bits) % m;
+    while (!is_prime(q)) q += m;
+    return q;
+}
+static uint64_t next_prime(uint64_t q, uint64_t m) {
+    do q += m;
+    while (!is_prime(q));
+    return q;
+}
+static uint64_t previous_prime(uint64_t q, uint64_t m) {
+    do q -= m;
+    while (!is_prime(q));
+    return q;
+}
+static uint64_t root_of_unity(uint64_t m, uint64_t q) {  // minimal primitive m-th root
+    uint64_t psi = 0;
+    for (uint64_t c = 2;; c++) {
+        psi = powmod(c, (q - 1) / m, q);
+        if (powmod(psi, m / 2, q) == q - 1) break;
+    }
+    uint64_t best = psi, x = psi, p2 = mulmod(psi, psi, q);
+    for (uint64_t k = 3; k < m; k += 2) {
+        x = mulmod(x, p2, q);
+        if (x < best) best = x;
+    }
+    return best;
+}
+static std::shared_ptr<DCRTParams> params(uint32_t m, const std::vector<uint64_t>& q) {
+    std::vector<uint64_t> r;
+    for (auto x : q) r.push_back(root_of_unity(m, x));
+    return std::make_shared<DCRTParams>(m, q, r);
+}
+
+static void TEST(const char* name, const std::function<void()>& f) {
+    int before = g_fail;
+    g_run++;
+    try {
+        f();
+    } catch (const std::exception& e) {
+        std::printf("  FAIL %s: exception %s\n", name, e.what());
+        g_fail++;
+    }
+    std::printf("[%s] %s\n", g_fail == before ? "  OK  " : " FAIL ", name);
+}
+
+int main() {
+    // UnitTestTransform.cpp:60-94
+    TEST("UTTransform.CRT_polynomial_mult", [] {
+        auto P = params(8, {113});
+        EXPECT_EQ(P->Roots()[0], 18u, "RootOfUnity(8, 113)");
+        DCRTPolyHip a(P, Format::COEFFICIENT);
+        a.SetValues({1, 2, 4, 1}, Format::COEFFICIENT);
+        a.SwitchFormat();
+        DCRTPolyHip ab = a.Times(a);
+        ab.SwitchFormat();
+        EXPECT_EQ(ab.GetValues(), (std::vector<uint64_t>{94, 109, 11, 18}), "inverse transform");
+    });
+    // UnitTestNTT.cpp:53-86
+    TEST("UTNTT.switch_format_simple_single_crt", [] {
+        auto P = params(16, {first_prime(22, 16)});
+        DCRTPolyHip x1(P, Format::COEFFICIENT);
+        std::vector<uint64_t> v{431, 3414, 1234, 7845, 2145, 7415, 5471, 8452};
+        x1.SetValues(v, Format::COEFFICIENT);
+        DCRTPolyHip clone(x1);
+        x1.SwitchFormat();
+        x1.SwitchFormat();
+        EXPECT_EQ(x1, clone, "round trip");
+        EXPECT_EQ(x1.GetValues(), v, "values");
+    });
+    // UnitTestNTT.cpp:88-133
+    TEST("UTNTT.switch_format_simple_double_crt", [] {
+        uint64_t q0 = first_prime(28, 16);
+        auto P = params(16, {q0, next_prime(q0, 16)});
+        DCRTPolyHip x(P, Format::COEFFICIENT);
+        std::vector<uint64_t> v{4127, 9647, 1987, 5410, 6541, 7014, 9741, 1256};
+        std::vector<uint64_t> both(v);
+        both.insert(both.end(), v.begin(), v.end());
+        x.SetValues(both, Format::COEFFICIENT);
+        x.SwitchFormat();
+        x.SwitchFormat();
+        EXPECT_EQ(x.GetValues(), both, "round trip");
+    });
+    // UnitTestMubintvec.cpp:276-359
+    TEST("UTmubintvec.basic_vector_vector_mod_math_1_limb", [] {
+        auto P = params(32, {163841});
+        std::vector<uint64_t> a{127753, 77706, 17133, 22582, 112132, 27625, 126773, 8924,
+                                125972, 2551, 113837, 112045, 100953, 77352, 132013, 57029};
+        std::vector<uint64_t> b{66773, 69572, 142134, 141115, 123182, 155822, 128147, 94818,
+                                135782, 30844, 88634, 99407, 53647, 111689, 28502, 26401};
+        DCRTPolyHip A(P, Format::EVALUATION), B(P, Format::EVALUATION);
+        A.SetValues(a, Format::EVALUATION);
+        B.SetValues(b, Format::EVALUATION);
+        EXPECT_EQ((A + B).GetValues(),
+                  (std::vector<uint64_t>{30685, 147278, 159267, 163697, 71473, 19606, 91079, 103742, 97913, 33395,
+                                         38630, 47611, 154600, 25200, 160515, 83430}),
+                  "ModAdd");
+        EXPECT_EQ((A - B).GetValues(),
+                  (std::vector<uint64_t>{60980, 8134, 38840, 45308, 152791, 35644, 162467, 77947, 154031, 135548,
+                                         25203, 12638, 47306, 129504, 103511, 30628}),
+                  "ModSub");
+        DCRTPolyHip D(A);
+        D *= B;
+        EXPECT_EQ(D.GetValues(),
+                  (std::vector<uint64_t>{69404, 64196, 13039, 115321, 28519, 151998, 89117, 80908, 57386, 39364, 8355,
+                                         146135, 61336, 31598, 25961, 87680}),
+                  "ModMul *=");
+    });
+    // UnitTestDCRTElements.cpp:549-590 (property oracle: (a op b).Mod(q))
+    TEST("UTDCRTPoly.DCRT_mod_ops_on_two_elements", [] {
+        std::vector<uint64_t> q{first_prime(24, 16)};
+        q.push_back(next_prime(q[0], 16));
+        q.push_back(next_prime(q[1], 16));
+        auto P = params(16, q);
+        std::mt19937_64 rng(11);
+        std::vector<uint64_t> a(24), b(24);
+        for (size_t i = 0; i < 24; i++) a[i] = rng() % q[i / 8], b[i] = rng() % q[i / 8];
+        DCRTPolyHip A(P, Format::EVALUATION), B(P, Format::EVALUATION);
+        A.SetValues(a, Format::EVALUATION);
+        B.SetValues(b, Format::EVALUATION);
+        auto s = (A + B).GetValues(), p = (A * B).GetValues();
+        for (size_t i = 0; i < 24; i++) {
+            EXPECT_EQ(s[i], (a[i] + b[i]) % q[i / 8], "sum index " + std::to_string(i));
+            EXPECT_EQ(p[i], (uint64_t)((u128)a[i] * b[i] % q[i / 8]), "prod index " + std::to_string(i));
+        }
+    });
+    // DCRTPoly SwitchFormat -> Times -> SwitchFormat vs the fused kernel, N = 2^14, 8 towers
+    TEST("DCRTPolyHip.pipeline_matches_switchformat_times", [] {
+        const uint32_t m = 1u << 15;
+        std::vector<uint64_t> q;
+        uint64_t x = first_prime(60, m);
+        for (int t = 0; t < 8; t++) q.push_back(x = previous_prime(x, m));
+        auto P = params(m, q);
+        std::mt19937_64 rng(3);
+        const uint32_t batch = 2;
+        std::vector<uint64_t> a((size_t)batch * 8 * (m / 2)), b(a.size());
+        for (size_t i = 0; i < a.size(); i++) {
+            const uint64_t qt = q[(i / (m / 2)) % 8];
+            a[i] = rng() % qt;
+            b[i] = rng() % qt;
+        }
+        DCRTPolyHip A(P, Format::COEFFICIENT, batch), B(P, Format::EVALUATION, batch);
+        A.SetValues(a, Format::COEFFICIENT);
+        B.SetValues(b, Format::EVALUATION);
+        DCRTPolyHip fused = A.MulViaNTT(B);
+        DCRTPolyHip step(A);
+        step.SwitchFormat();
+        step *= B;
+        step.SwitchFormat();
+        EXPECT_EQ(fused, step, "fused vs step-by-step");
+        // scalar Times (mubintvecnat.cpp:310-332) vs host
+        std::vector<uint64_t> sc;
+        for (int t = 0; t < 8; t++) sc.push_back(rng());
+        auto r = A.Times(sc).GetValues();
+        bool ok = true;
+        for (size_t i = 0; i < a.size(); i++) {
+            const size_t t = (i / (m / 2)) % 8;
+            ok = ok && r[i] == (uint64_t)((u128)a[i] * (sc[t] % q[t]) % q[t]);
+        }
+        EXPECT_EQ(ok, true, "scalar Times");
+    });
+    // error behaviour: OPENFHE_THROW analogues
+    TEST("DCRTPolyHip.errors", [] {
+        auto P = params(16, {first_prime(22, 16)});
+        auto P2 = params(16, {next_prime(first_prime(22, 16), 16)});
+        DCRTPolyHip a(P, Format::COEFFICIENT), b(P, Format::COEFFICIENT), c(P2, Format::EVALUATION);
+        EXPECT_THROW(a.Times(b), not_implemented_error, "Times in COEFFICIENT");
+        DCRTPolyHip e(P, Format::EVALUATION);
+        EXPECT_THROW(e.Times(c), math_error, "Modulus missmatch");
+        EXPECT_THROW(DCRTParams(12, {17}, {3}), math_error, "non power of two order");
+        EXPECT_THROW(DCRTParams(16, {first_prime(22, 16) + 2}, {3}), math_error, "bad modulus");
+    });
+    std::printf("%d tests, %d failures\n", g_run, g_fail);
+    return g_fail ? 1 : 0;
+}

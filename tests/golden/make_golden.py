@@ -1,0 +1,152 @@
+"""Generates tests/golden/*.json.
+
+Two kinds of fixture live here:
+
+1. Vectors copied as DATA from the reference's own unit tests and from the
+   reference-run probe results recorded in SURVEY.md §8(c) (the reference's
+   native code, compiled during the survey, run on the inputs described
+   there).  These pin the oracle:
+     - UnitTestTransform.cpp:60-94  CRT_polynomial_mult KAT (q=113, m=8)
+     - UnitTestMubintvec.cpp:276-359 1-limb vector ModAdd/ModSub/ModMul KAT
+     - UnitTestNTT.cpp:53-133 round-trip inputs
+     - SURVEY.md §8(c) probe outputs (moduli, minimal roots, y[0], y[1], c[0][0])
+2. Oracle outputs (oracle/ofhe_oracle.c) at small sizes, used as committed
+   golden vectors for the GPU parity tests (regenerate with this script; the
+   oracle is itself checked against the fixtures of kind 1 in
+   tests/test_oracle.py).
+
+Run:  python tests/golden/make_golden.py
+"""
+import json
+import os
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+import oracle as O  # noqa: E402
+
+
+def reference_fixtures():
+    return {
+        "source": "reference unit tests + SURVEY.md §8(c) probe outputs",
+        "kat_transform": {
+            "ref": "src/core/unittest/UnitTestTransform.cpp:60-94",
+            "q": 113, "m": 8, "a": [1, 2, 4, 1], "expected": [94, 109, 11, 18], "root": 18,
+        },
+        "kat_mubintvec": {
+            "ref": "src/core/unittest/UnitTestMubintvec.cpp:276-359",
+            "q": 163841,
+            "a": [127753, 77706, 17133, 22582, 112132, 27625, 126773, 8924,
+                  125972, 2551, 113837, 112045, 100953, 77352, 132013, 57029],
+            "b": [66773, 69572, 142134, 141115, 123182, 155822, 128147, 94818,
+                  135782, 30844, 88634, 99407, 53647, 111689, 28502, 26401],
+            "modadd": [30685, 147278, 159267, 163697, 71473, 19606, 91079, 103742,
+                       97913, 33395, 38630, 47611, 154600, 25200, 160515, 83430],
+            "modsub": [60980, 8134, 38840, 45308, 152791, 35644, 162467, 77947,
+                       154031, 135548, 25203, 12638, 47306, 129504, 103511, 30628],
+            "modmul": [69404, 64196, 13039, 115321, 28519, 151998, 89117, 80908,
+                       57386, 39364, 8355, 146135, 61336, 31598, 25961, 87680],
+        },
+        "roundtrip_ntt": {
+            "ref": "src/core/unittest/UnitTestNTT.cpp:53-133",
+            "m": 16,
+            "x1": [431, 3414, 1234, 7845, 2145, 7415, 5471, 8452],
+            "x2": [4127, 9647, 1987, 5410, 6541, 7014, 9741, 1256],
+            "single_crt_bits": 22, "double_crt_bits": 28,
+        },
+        "survey_probes": {
+            "ref": "SURVEY.md §8(c) (reference native code run in the survey container)",
+            "rng": "splitmix64, state += 0x9E3779B97F4A7C15; x_i = sm() % q in index order",
+            "ntt": [
+                {"log_n": 14, "tower": 0, "seed": 42, "q": 1152921504606748673, "psi": 62213374832584,
+                 "y0": 698053391994828643, "y1": 668512656094057990},
+                {"log_n": 14, "tower": 1, "seed": 43, "q": 1152921504606683137, "psi": 212089012217363},
+                {"log_n": 16, "tower": 0, "seed": 42, "q": 1152921504606584833, "psi": 18043022392882,
+                 "y0": 1114074043317201401},
+                {"log_n": 16, "tower": 1, "seed": 43, "q": 1152921504598720513, "psi": 800790938143},
+            ],
+            "dcrt_pipeline": {
+                "log_n": 14, "towers": 8, "seed": 1,
+                "draw": "one stream; for t: for i: a[t][i] = sm() % q_t; b[t][i] = sm() % q_t",
+                "op": "c = INTT(NTT(a) (.) b)", "c00": 866544996928583785,
+            },
+        },
+    }
+
+
+def fx(a):
+    return [int(v) for v in np.asarray(a).reshape(-1)]
+
+
+def oracle_vectors():
+    """Small full vectors from the oracle for GPU parity (N <= 2^12)."""
+    cases = []
+    for log_n, towers, batch in ((1, 2, 2), (3, 2, 2), (6, 3, 1), (10, 2, 2), (11, 1, 1)):
+        n = 1 << log_n
+        qs, rs = O.moduli_chain(log_n, towers)
+        tb = O.Tables(n, qs, rs)
+        a = O.uniform_dcrt(batch, towers, n, qs, seed=1)
+        b = O.uniform_dcrt(batch, towers, n, qs, seed=2)
+        cases.append({
+            "log_n": log_n, "towers": towers, "batch": batch, "q": qs, "psi": rs,
+            "a": fx(a), "b": fx(b),
+            "ntt_a": fx(O.ntt_fwd(a, tb)),
+            "intt_a": fx(O.ntt_inv(a, tb)),
+            "mul": fx(O.eltwise("mul", a, b, qs)),
+            "add": fx(O.eltwise("add", a, b, qs)),
+            "sub": fx(O.eltwise("sub", a, b, qs)),
+            "pipeline": fx(O.ntt_mul_intt(a, b, tb)),
+        })
+    return {"source": "oracle/ofhe_oracle.c via tests/golden/make_golden.py", "cases": cases}
+
+
+def oracle_fingerprints():
+    """FNV-1a fingerprints of oracle outputs at the benchmark shapes (GPU parity
+    at full size without shipping megabytes of vectors)."""
+    out = []
+    for log_n, towers, batch in ((12, 2, 2), (13, 3, 2), (14, 8, 1), (15, 2, 1), (16, 4, 1), (17, 2, 1)):
+        n = 1 << log_n
+        qs, rs = O.moduli_chain(log_n, towers)
+        tb = O.Tables(n, qs, rs)
+        a = O.uniform_dcrt(batch, towers, n, qs, seed=11)
+        b = O.uniform_dcrt(batch, towers, n, qs, seed=12)
+        out.append({
+            "log_n": log_n, "towers": towers, "batch": batch, "q": qs, "psi": rs,
+            "seed_a": 11, "seed_b": 12,
+            "fnv_ntt_a": O.fnv64(O.ntt_fwd(a, tb)),
+            "fnv_intt_a": O.fnv64(O.ntt_inv(a, tb)),
+            "fnv_mul": O.fnv64(O.eltwise("mul", a, b, qs)),
+            "fnv_pipeline": O.fnv64(O.ntt_mul_intt(a, b, tb)),
+        })
+    return {"source": "oracle/ofhe_oracle.c via tests/golden/make_golden.py", "fingerprints": out}
+
+
+def bconv_vectors():
+    out = []
+    for log_n, sq, sp, batch in ((4, 3, 2, 2), (9, 5, 4, 1), (10, 2, 11, 1)):
+        n = 1 << log_n
+        chain, _ = O.moduli_chain(log_n, sq + sp)
+        q, p = chain[:sq], chain[sq:]
+        pre = O.base_conv_precompute(q, p)
+        x = O.uniform_dcrt(batch, sq, n, q, seed=5)
+        y = np.stack([O.approx_switch_crt_basis(x[bi], q, p, pre) for bi in range(batch)])
+        out.append({"log_n": log_n, "batch": batch, "q": q, "p": p, "qhat_inv_modq": fx(pre["qhinv"]),
+                    "qhat_modp": fx(pre["qhmodp"]), "x": fx(x), "out": fx(y)})
+    return {"source": "oracle/ofhe_oracle.c via tests/golden/make_golden.py", "cases": out}
+
+
+def main():
+    for name, obj in (("reference_fixtures.json", reference_fixtures()),
+                      ("oracle_vectors.json", oracle_vectors()),
+                      ("oracle_fingerprints.json", oracle_fingerprints()),
+                      ("bconv_vectors.json", bconv_vectors())):
+        with open(os.path.join(HERE, name), "w") as f:
+            json.dump(obj, f, separators=(",", ":"))
+        print("wrote", name, os.path.getsize(os.path.join(HERE, name)), "bytes")
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,272 @@
+"""GPU parity: the HIP backend (through the C ABI) against the oracle and the
+committed golden vectors.  Bit-exact for every op (integer arithmetic).
+
+Mirrors the reference's own tests: UnitTestTransform (KAT), UnitTestNTT
+(round trips), UnitTestMubintvec (vector ModAdd/ModSub/ModMul KATs),
+UnitTestDCRTElements (random DCRTPoly + and * against an independent check).
+"""
+import numpy as np
+import pytest
+from conftest import load_golden
+
+pytestmark = pytest.mark.gpu
+
+REF = load_golden("reference_fixtures.json")
+
+
+def dev(x):
+    import torch
+
+    return torch.from_numpy(np.ascontiguousarray(x, dtype=np.uint64).view(np.int64)).cuda()
+
+
+def host(t):
+    import torch
+
+    torch.cuda.synchronize()
+    return t.cpu().numpy().view(np.uint64)
+
+
+def stream():
+    import torch
+
+    return torch.cuda.current_stream().cuda_stream
+
+
+def run_all_ops(hip, plan, a, b):
+    """Every plan op on device copies of a, b -> dict of host results."""
+    import torch
+
+    out = {}
+    x = dev(a)
+    plan.forward(x.data_ptr(), a.shape[0], stream())
+    out["ntt_a"] = host(x)
+    x = dev(a)
+    plan.inverse(x.data_ptr(), a.shape[0], stream())
+    out["intt_a"] = host(x)
+    for op in ("mul", "add", "sub"):
+        xa, xb = dev(a), dev(b)
+        xc = torch.empty_like(xa)
+        getattr(plan, "mod_" + op)(xa.data_ptr(), xb.data_ptr(), xc.data_ptr(), a.shape[0], stream())
+        out[op] = host(xc)
+    xa, xb = dev(a), dev(b)
+    xc = torch.empty_like(xa)
+    plan.ntt_mul_intt(xa.data_ptr(), xb.data_ptr(), xc.data_ptr(), a.shape[0], stream())
+    out["pipeline"] = host(xc)
+    return out
+
+
+def test_kat_transform(hip):
+    """UnitTestTransform.cpp:60-94 on the GPU: [1,2,4,1]^2 mod (x^4+1, 113) = [94,109,11,18]."""
+    H, ctx = hip
+    k = REF["kat_transform"]
+    plan = H.NTTPlan(ctx, 2, [k["q"]], [k["root"]])
+    a = np.array(k["a"], np.uint64).reshape(1, 1, 4)
+    x = dev(a)
+    plan.forward(x.data_ptr(), 1, stream())
+    y = dev(np.zeros_like(a))
+    plan.mod_mul(x.data_ptr(), x.data_ptr(), y.data_ptr(), 1, stream())
+    plan.inverse(y.data_ptr(), 1, stream())
+    assert host(y).reshape(-1).tolist() == k["expected"]
+    # same through the fused pipeline (b = NTT(a))
+    c = dev(np.zeros_like(a))
+    plan.ntt_mul_intt(dev(a).data_ptr(), x.data_ptr(), c.data_ptr(), 1, stream())
+    assert host(c).reshape(-1).tolist() == k["expected"]
+
+
+def test_kat_mubintvec(hip):
+    """UnitTestMubintvec.cpp:276-359 (q = 163841) through the element-wise kernels."""
+    import torch
+
+    H, ctx = hip
+    k = REF["kat_mubintvec"]
+    q = k["q"]
+    # q = 163841 = 1 mod 2^15: a valid NTT modulus for N = 16; root from the oracle rule
+    psi = next(r for r in range(2, q) if pow(r, 16, q) == q - 1)
+    psi = min(pow(psi, e, q) for e in range(1, 32, 2))
+    plan = H.NTTPlan(ctx, 4, [q], [psi])
+    a, b = dev(np.array(k["a"], np.uint64)), dev(np.array(k["b"], np.uint64))
+    for op in ("add", "sub", "mul"):
+        c = torch.empty_like(a)
+        getattr(plan, "mod_" + op)(a.data_ptr(), b.data_ptr(), c.data_ptr(), 1, stream())
+        assert host(c).tolist() == k["mod" + op], op
+
+
+@pytest.mark.parametrize("case", range(5))
+def test_golden_vectors(hip, case):
+    H, ctx = hip
+    c = load_golden("oracle_vectors.json")["cases"][case]
+    n, T, B = 1 << c["log_n"], c["towers"], c["batch"]
+    plan = H.NTTPlan(ctx, c["log_n"], c["q"], c["psi"])
+    a = np.array(c["a"], np.uint64).reshape(B, T, n)
+    b = np.array(c["b"], np.uint64).reshape(B, T, n)
+    got = run_all_ops(H, plan, a, b)
+    for key in ("ntt_a", "intt_a", "mul", "add", "sub", "pipeline"):
+        assert got[key].reshape(-1).tolist() == c[key], key
+
+
+@pytest.mark.parametrize("idx", range(6))
+def test_fingerprints_full_size(hip, O, idx):
+    """Benchmark shapes (N = 2^12 .. 2^17): FNV-1a of every output equals the
+    committed oracle fingerprint, and the oracle run here agrees element-wise."""
+    H, ctx = hip
+    f = load_golden("oracle_fingerprints.json")["fingerprints"][idx]
+    n, T, B = 1 << f["log_n"], f["towers"], f["batch"]
+    plan = H.NTTPlan(ctx, f["log_n"], f["q"], f["psi"])
+    a = O.uniform_dcrt(B, T, n, f["q"], f["seed_a"])
+    b = O.uniform_dcrt(B, T, n, f["q"], f["seed_b"])
+    got = run_all_ops(H, plan, a, b)
+    assert O.fnv64(got["ntt_a"]) == f["fnv_ntt_a"]
+    assert O.fnv64(got["intt_a"]) == f["fnv_intt_a"]
+    assert O.fnv64(got["mul"]) == f["fnv_mul"]
+    assert O.fnv64(got["pipeline"]) == f["fnv_pipeline"]
+
+
+def test_survey_probe_dcrt_pipeline(hip, O):
+    """Reference output: DCRTPoly N=2^14, T=8, c[0][0]."""
+    import torch
+
+    H, ctx = hip
+    pr = REF["survey_probes"]["dcrt_pipeline"]
+    n, T = 1 << pr["log_n"], pr["towers"]
+    qs, rs = O.moduli_chain(pr["log_n"], T)
+    st = O.U([pr["seed"]])
+    a = np.zeros((1, T, n), np.uint64)
+    b = np.zeros((1, T, n), np.uint64)
+    for t in range(T):
+        ab = O.splitmix_fill(2 * n, qs[t], st)
+        a[0, t], b[0, t] = ab[0::2], ab[1::2]
+    plan = H.NTTPlan(ctx, pr["log_n"], qs, rs)
+    xa, xb = dev(a), dev(b)
+    xc = torch.empty_like(xa)
+    plan.ntt_mul_intt(xa.data_ptr(), xb.data_ptr(), xc.data_ptr(), 1, stream())
+    c = host(xc)
+    assert int(c[0, 0, 0]) == pr["c00"]
+    assert np.array_equal(c, O.ntt_mul_intt(a, b, O.Tables(n, qs, rs)))
+
+
+@pytest.mark.parametrize("log_n,towers,batch", [(1, 1, 3), (2, 3, 2), (5, 2, 4), (9, 4, 3), (11, 2, 2),
+                                                (12, 3, 3), (13, 1, 2), (14, 8, 2), (15, 3, 1), (16, 2, 2),
+                                                (17, 1, 2)])
+def test_random_shapes_vs_oracle(hip, O, log_n, towers, batch):
+    """Element-wise equality with the oracle over ragged (batch, tower) shapes."""
+    H, ctx = hip
+    n = 1 << log_n
+    qs, rs = O.moduli_chain(log_n, towers)
+    tb = O.Tables(n, qs, rs)
+    a = O.uniform_dcrt(batch, towers, n, qs, 100 + log_n)
+    b = O.uniform_dcrt(batch, towers, n, qs, 200 + log_n)
+    got = run_all_ops(H, H.NTTPlan(ctx, log_n, qs, rs), a, b)
+    assert np.array_equal(got["ntt_a"], O.ntt_fwd(a, tb))
+    assert np.array_equal(got["intt_a"], O.ntt_inv(a, tb))
+    assert np.array_equal(got["mul"], O.eltwise("mul", a, b, qs))
+    assert np.array_equal(got["pipeline"], O.ntt_mul_intt(a, b, tb))
+
+
+def test_edge_values(hip, O):
+    """All-zero, all-(q-1) and alternating extreme inputs (lazy-reduction corners)."""
+    H, ctx = hip
+    log_n, T = 14, 3
+    n = 1 << log_n
+    qs, rs = O.moduli_chain(log_n, T)
+    tb = O.Tables(n, qs, rs)
+    q = np.array(qs, np.uint64)[None, :, None]
+    for a in (np.zeros((1, T, n), np.uint64), np.broadcast_to(q - np.uint64(1), (1, T, n)).copy(),
+              np.where(np.arange(n) % 2 == 0, q - np.uint64(1), np.uint64(0)).astype(np.uint64)):
+        b = np.broadcast_to(q - np.uint64(1), (1, T, n)).copy()
+        got = run_all_ops(H, H.NTTPlan(ctx, log_n, qs, rs), a, b)
+        assert np.array_equal(got["ntt_a"], O.ntt_fwd(a, tb))
+        assert np.array_equal(got["intt_a"], O.ntt_inv(a, tb))
+        assert np.array_equal(got["pipeline"], O.ntt_mul_intt(a, b, tb))
+
+
+def test_inplace_and_roundtrip_full_size(hip, O):
+    """N = 2^16, T = 16: INTT(NTT(x)) = x in place; fused op with c aliasing a;
+    linearity NTT(a + b) = NTT(a) + NTT(b)."""
+    import torch
+
+    H, ctx = hip
+    log_n, T, B = 16, 16, 2
+    n = 1 << log_n
+    qs, rs = O.moduli_chain(log_n, T)
+    plan = H.NTTPlan(ctx, log_n, qs, rs)
+    a = O.uniform_dcrt(B, T, n, qs, 77)
+    b = O.uniform_dcrt(B, T, n, qs, 78)
+    x = dev(a)
+    plan.forward(x.data_ptr(), B, stream())
+    plan.inverse(x.data_ptr(), B, stream())
+    assert np.array_equal(host(x), a)
+    xa, xb = dev(a), dev(b)
+    plan.ntt_mul_intt(xa.data_ptr(), xb.data_ptr(), xa.data_ptr(), B, stream())
+    assert np.array_equal(host(xa), O.ntt_mul_intt(a, b, O.Tables(n, qs, rs)))
+    xa, xb, xs = dev(a), dev(b), torch.empty_like(dev(a))
+    plan.mod_add(xa.data_ptr(), xb.data_ptr(), xs.data_ptr(), B, stream())
+    for t_ in (xa, xb, xs):
+        plan.forward(t_.data_ptr(), B, stream())
+    s2 = torch.empty_like(xs)
+    plan.mod_add(xa.data_ptr(), xb.data_ptr(), s2.data_ptr(), B, stream())
+    assert np.array_equal(host(xs), host(s2))
+
+
+def test_scalar_modmul(hip, O):
+    import torch
+
+    H, ctx = hip
+    log_n, T, B = 12, 3, 2
+    n = 1 << log_n
+    qs, rs = O.moduli_chain(log_n, T)
+    plan = H.NTTPlan(ctx, log_n, qs, rs)
+    a = O.uniform_dcrt(B, T, n, qs, 5)
+    sc = [qs[0] - 1, 12345678901234567, 2**63 + 5]  # the last is reduced mod q first
+    x = dev(a)
+    y = torch.empty_like(x)
+    plan.mod_mul_scalar(x.data_ptr(), sc, y.data_ptr(), B, stream())
+    assert np.array_equal(host(y), O.mul_scalar(a, [s % q for s, q in zip(sc, qs)], qs))
+
+
+@pytest.mark.parametrize("case", range(3))
+def test_base_conversion_golden(hip, O, case):
+    import torch
+
+    H, ctx = hip
+    c = load_golden("bconv_vectors.json")["cases"][case]
+    n, B, sq, sp = 1 << c["log_n"], c["batch"], len(c["q"]), len(c["p"])
+    bc = H.BaseConverter(ctx, c["log_n"], c["q"], c["p"], c["qhat_inv_modq"], c["qhat_modp"])
+    x = dev(np.array(c["x"], np.uint64).reshape(B, sq, n))
+    out = torch.zeros((B, sp, n), dtype=torch.int64, device="cuda")
+    bc.switch(x.data_ptr(), out.data_ptr(), B, stream())
+    assert host(out).reshape(-1).tolist() == c["out"]
+
+
+def test_base_conversion_config5_shape(hip, O):
+    """N = 2^17 digit -> complement (16 -> 17 towers), vs the oracle."""
+    import torch
+
+    H, ctx = hip
+    log_n, sq, sp = 17, 16, 17
+    n = 1 << log_n
+    chain, _ = O.moduli_chain(log_n, sq + sp)
+    q, p = chain[:sq], chain[sq:]
+    pre = O.base_conv_precompute(q, p)
+    x = O.uniform_dcrt(1, sq, n, q, 31)
+    bc = H.BaseConverter(ctx, log_n, q, p, [int(v) for v in pre["qhinv"]], [int(v) for v in pre["qhmodp"]])
+    out = torch.zeros((1, sp, n), dtype=torch.int64, device="cuda")
+    bc.switch(dev(x).data_ptr(), out.data_ptr(), 1, stream())
+    assert np.array_equal(host(out)[0], O.approx_switch_crt_basis(x[0], q, p, pre))
+
+
+def test_errors_raise(hip, O):
+    """Invalid parameters fail loudly (math_error analogue), as OPENFHE_THROW does."""
+    H, ctx = hip
+    qs, rs = O.moduli_chain(10, 1)
+    with pytest.raises(H.MathError):
+        H.NTTPlan(ctx, 10, [qs[0]], [1])               # root 1 is not primitive
+    with pytest.raises(H.MathError):
+        H.NTTPlan(ctx, 10, [qs[0] + 2], [rs[0]])       # not 1 mod 2N
+    with pytest.raises(H.MathError):
+        H.NTTPlan(ctx, 18, qs, rs)                     # ring too large
+    plan = H.NTTPlan(ctx, 10, qs, rs)
+    with pytest.raises(H.MathError):
+        plan.forward(0, 1, stream())                   # NULL data
+    with pytest.raises(H.MathError):
+        plan.forward(1 << 20, 0, stream())             # empty batch

@@ -1,0 +1,120 @@
+// arith.hpp -- 64-bit modular arithmetic for gfx950 (device side).
+//
+// gfx950 has no 64x64 multiplier: every u64 product is built from the
+// quarter-rate v_mad_u64_u32 / v_mul_lo_u32 / v_mul_hi_u32 (measured
+// ~18 T lane-ops/s each vs ~70 T for full-rate VALU, tools/microbench).
+// The NTT is therefore VALU(multiply)-bound, and these helpers are written
+// to minimise multiplies:
+//   * mulhi_approx: floor(a*b/2^64) - {0,1} with 3 mads (drops the a0*b0
+//     carry, Harvey-style slack absorbed by lazy reduction);
+//   * shoup_lazy: a*w mod q in [0, 3q) (Shoup / Harvey, "FASTER ARITHMETIC FOR
+//     NUMBER-THEORETIC TRANSFORMS"; reference: ubintnat.h:1478-1497 computes
+//     the canonical form);
+//   * barrett_ref: bit-exact restatement of NativeIntegerT::ModMulFastEq
+//     (ubintnat.h:1399-1413), used for the vector x vector Hadamard product.
+// All moduli satisfy q < 2^60 (OpenFHE MAX_MODULUS_SIZE = 60, basicint.h:44),
+// so lazy values up to 8q < 2^63 never overflow.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace ofhe {
+
+typedef uint64_t u64;
+typedef uint32_t u32;
+
+__device__ __forceinline__ u32 lo32(u64 x) { return (u32)x; }
+__device__ __forceinline__ u32 hi32(u64 x) { return (u32)(x >> 32); }
+
+// v_mad_u64_u32: a*b + c, exact in 64 bits for 32-bit a, b, c < 2^64 - (2^32-1)^2
+__device__ __forceinline__ u64 mad32(u32 a, u32 b, u64 c) { return (u64)a * (u64)b + c; }
+
+// floor(a*b / 2^64) or one less.  3 x v_mad_u64_u32 + one 64-bit add.
+__device__ __forceinline__ u64 mulhi_approx(u64 a, u64 b) {
+    u64 m1 = mad32(lo32(a), hi32(b), 0);
+    u64 m2 = mad32(hi32(a), lo32(b), (u64)lo32(m1));
+    u64 h = mad32(hi32(a), hi32(b), (u64)hi32(m1));
+    return h + (u64)hi32(m2);
+}
+
+// exact floor(a*b / 2^64)
+__device__ __forceinline__ u64 mulhi_exact(u64 a, u64 b) {
+    u64 p00 = mad32(lo32(a), lo32(b), 0);
+    u64 m1 = mad32(lo32(a), hi32(b), (u64)hi32(p00));
+    u64 m2 = mad32(hi32(a), lo32(b), (u64)lo32(m1));
+    u64 h = mad32(hi32(a), hi32(b), (u64)hi32(m1));
+    return h + (u64)hi32(m2);
+}
+
+// low 64 bits of a*b: 1 mad + 2 mul_lo (folded into mads by the compiler)
+__device__ __forceinline__ u64 mullo(u64 a, u64 b) { return a * b; }
+
+// Shoup with precomputed wp = floor(w*2^64/q): a*w mod q in [0, 3q) for any a < 2^64.
+__device__ __forceinline__ u64 shoup_lazy(u64 a, u64 w, u64 wp, u64 q) {
+    u64 qh = mulhi_approx(a, wp);
+    return a * w - qh * q;
+}
+
+__device__ __forceinline__ u64 csub(u64 x, u64 m) { return x >= m ? x - m : x; }
+
+// canonical Shoup: ModMulFastConstEq semantics (result in [0, q)).
+__device__ __forceinline__ u64 shoup_canon(u64 a, u64 w, u64 wp, u64 q) {
+    u64 r = shoup_lazy(a, w, wp, q);
+    r = csub(r, 2 * q);
+    return csub(r, q);
+}
+
+// NativeIntegerT::ModMulFastEq(b, q, mu), ubintnat.h:1399-1413, bit for bit:
+//   prod = a*b (128-bit); n = msb(q) - 2;
+//   est  = ((prod >> n) * mu) >> (n + 7);   r = lo64(prod - q*est); r -= q if r >= q.
+// n_shift = msb(q) - 2 is passed in (per tower constant).
+__device__ __forceinline__ u64 barrett_ref(u64 a, u64 b, u64 q, u64 mu, u32 n_shift) {
+    // 128-bit product
+    u64 p00 = mad32(lo32(a), lo32(b), 0);
+    u64 m1 = mad32(lo32(a), hi32(b), (u64)hi32(p00));
+    u64 m2 = mad32(hi32(a), lo32(b), (u64)lo32(m1));
+    u64 hi = mad32(hi32(a), hi32(b), (u64)hi32(m1)) + (u64)hi32(m2);
+    u64 lo = ((u64)lo32(m2) << 32) | lo32(p00);
+    // (prod >> n) truncated to 64 bits (n in [0, 62])
+    u64 sh = n_shift ? ((lo >> n_shift) | (hi << (64 - n_shift))) : lo;
+    // (sh * mu) >> (n + 7): 128-bit product then shift
+    u64 q00 = mad32(lo32(sh), lo32(mu), 0);
+    u64 r1 = mad32(lo32(sh), hi32(mu), (u64)hi32(q00));
+    u64 r2 = mad32(hi32(sh), lo32(mu), (u64)lo32(r1));
+    u64 th = mad32(hi32(sh), hi32(mu), (u64)hi32(r1)) + (u64)hi32(r2);
+    u64 tl = ((u64)lo32(r2) << 32) | lo32(q00);
+    u32 s = n_shift + 7;  // in [7, 69]
+    u64 est = s >= 64 ? (th >> (s - 64)) : ((tl >> s) | (th << (64 - s)));
+    u64 r = lo - est * q;
+    return r >= q ? r - q : r;
+}
+
+// Exact 64x64 -> 128 product (for base conversion accumulation).
+__device__ __forceinline__ void mul128(u64 a, u64 b, u64& lo, u64& hi) {
+    u64 p00 = mad32(lo32(a), lo32(b), 0);
+    u64 m1 = mad32(lo32(a), hi32(b), (u64)hi32(p00));
+    u64 m2 = mad32(hi32(a), lo32(b), (u64)lo32(m1));
+    hi = mad32(hi32(a), hi32(b), (u64)hi32(m1)) + (u64)hi32(m2);
+    lo = ((u64)lo32(m2) << 32) | lo32(p00);
+}
+
+// BarrettUint128ModUint64, utils/utilities-int.h:61-103 (exact value; the
+// final while-loop makes it canonical).  mu = floor(2^128 / m).
+__device__ __forceinline__ u64 barrett128(u64 a_lo, u64 a_hi, u64 m, u64 mu_lo, u64 mu_hi) {
+    u64 left_hi = mulhi_exact(a_lo, mu_lo);
+    u64 mid_lo, mid_hi;
+    mul128(a_lo, mu_hi, mid_lo, mid_hi);
+    u64 tmp1 = mid_lo + left_hi;
+    u64 carry = tmp1 < mid_lo;
+    u64 tmp2 = mid_hi + carry;
+    mul128(a_hi, mu_lo, mid_lo, mid_hi);
+    u64 s = mid_lo + tmp1;
+    carry = s < mid_lo;
+    left_hi = mid_hi + carry;
+    tmp1 = a_hi * mu_hi + tmp2 + left_hi;
+    u64 r = a_lo - tmp1 * m;
+    while (r >= m) r -= m;
+    return r;
+}
+
+}  // namespace ofhe

@@ -1,0 +1,104 @@
+// eltwise_kernels.hpp -- coefficient-wise RNS ops and base conversion (gfx950).
+//
+// Element-wise kernels are pure HBM streams (24 B per coefficient for a
+// vector-vector op): 16-byte loads/stores, grid-stride, one tower constant
+// set per polynomial.  They replace the DPU VECTOR/VECTOR_EQ kernels of
+// src/core/pim/dpu/element-wise/{add-mod,sub-mod,mult-mod}.c and the CPU loops
+// of NativeVectorT (mubintvecnat.cpp:245-367).
+#pragma once
+#include "ntt_kernels.hpp"
+
+namespace ofhe {
+
+enum { ELT_MUL = 0, ELT_ADD = 1, ELT_SUB = 2, ELT_MULS = 3 };
+
+// a, b, c: [batch][towers][N]; for ELT_MULS, b is a device array of
+// (s_t, s_t') pairs, one per tower.
+template <int OP>
+__global__ __launch_bounds__(256) void k_eltwise(const TowerConst* __restrict__ tcs,
+                                                 const u64* a, const u64* b, u64* c, u64 npairs,
+                                                 u32 log_n, u32 towers) {
+    const u64 stride = (u64)gridDim.x * blockDim.x;
+    for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < npairs; i += stride) {
+        const u64 e = 2 * i;
+        const u32 t = (u32)((e >> log_n) % towers);
+        const TowerConst tc = tcs[t];
+        const ulonglong2 x = reinterpret_cast<const ulonglong2*>(a)[i];
+        ulonglong2 r;
+        if (OP == ELT_MULS) {
+            const u64 s = b[2 * t], sp = b[2 * t + 1];
+            r.x = shoup_canon(x.x, s, sp, tc.q);
+            r.y = shoup_canon(x.y, s, sp, tc.q);
+        } else {
+            const ulonglong2 y = reinterpret_cast<const ulonglong2*>(b)[i];
+            if (OP == ELT_MUL) {
+                r.x = barrett_ref(x.x, y.x, tc.q, tc.mu, tc.nshift);
+                r.y = barrett_ref(x.y, y.y, tc.q, tc.mu, tc.nshift);
+            } else if (OP == ELT_ADD) {  // ModAddFastEq, ubintnat.h:760-767
+                r.x = csub(x.x + y.x, tc.q);
+                r.y = csub(x.y + y.y, tc.q);
+            } else {  // ModSubFastEq, ubintnat.h:934-938
+                r.x = x.x < y.x ? x.x + tc.q - y.x : x.x - y.x;
+                r.y = x.y < y.y ? x.y + tc.q - y.y : x.y - y.y;
+            }
+        }
+        reinterpret_cast<ulonglong2*>(c)[i] = r;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// ApproxSwitchCRTBasis (dcrtpoly-impl.h:1034-1063): per coefficient ri,
+//   y_i   = [x_i * QHatInvModq_i]_{q_i}                 (Shoup, canonical)
+//   s_j   = sum_i y_i * QHatModp_{i,j}                  (128-bit accumulate)
+//   out_j = BarrettUint128ModUint64(s_j, p_j, mu_j)     (canonical)
+// One thread per (batch, ri); the P side is processed in tiles of PT towers
+// so the 128-bit accumulators stay in registers.
+// ---------------------------------------------------------------------------
+struct BconvArgs {
+    const u64* qv;        // [sizeQ]
+    const u64* qhinv;     // [sizeQ][2]  (QHatInvModq, Shoup precon)
+    const u64* qhmodp;    // [sizeQ][sizeP]
+    const u64* pv;        // [sizeP]
+    const u64* pmu;       // [sizeP][2]  (mu_lo, mu_hi) = floor(2^128 / p)
+    u32 log_n, size_q, size_p;
+};
+
+template <int PT>
+__global__ __launch_bounds__(256) void k_bconv(BconvArgs A, const u64* __restrict__ x,
+                                               u64* __restrict__ out, u32 batch) {
+    const u32 N = 1u << A.log_n;
+    const u64 gid = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (gid >= (u64)batch * N) return;
+    const u32 b = (u32)(gid >> A.log_n), ri = (u32)(gid & (N - 1));
+    const u64* xb = x + (u64)b * A.size_q * N + ri;
+    u64* ob = out + (u64)b * A.size_p * N + ri;
+    for (u32 j0 = 0; j0 < A.size_p; j0 += PT) {
+        u64 lo[PT], hi[PT];
+#pragma unroll
+        for (int j = 0; j < PT; j++) lo[j] = hi[j] = 0;
+        const u32 jn = min((u32)PT, A.size_p - j0);
+        for (u32 i = 0; i < A.size_q; i++) {
+            const u64 y = shoup_canon(xb[(u64)i * N], A.qhinv[2 * i], A.qhinv[2 * i + 1], A.qv[i]);
+            const u64* qm = A.qhmodp + (u64)i * A.size_p + j0;
+#pragma unroll
+            for (int j = 0; j < PT; j++) {
+                if (j < (int)jn) {
+                    u64 pl, ph;
+                    mul128(y, qm[j], pl, ph);
+                    const u64 s = lo[j] + pl;
+                    hi[j] += ph + (s < pl);
+                    lo[j] = s;
+                }
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < PT; j++) {
+            if (j < (int)jn) {
+                const u32 jj = j0 + j;
+                ob[(u64)jj * N] = barrett128(lo[j], hi[j], A.pv[jj], A.pmu[2 * jj], A.pmu[2 * jj + 1]);
+            }
+        }
+    }
+}
+
+}  // namespace ofhe

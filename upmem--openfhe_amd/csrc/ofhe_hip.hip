@@ -1,0 +1,565 @@
+// ofhe_hip.hip -- C ABI (include/ofhe_hip.h) of the gfx950 RNS backend.
+//
+// Replaces the UPMEM interception layer of the reference:
+//   PimManager (src/core/include/pim/PimManager.h:21-127, pim/host/PimManager.cpp)
+//     -> ofhe_ctx_s: one per device; allocation and
+//        transfers are hipMalloc / hipMemcpyAsync instead of per-DPU MRAM
+//        chunks (DpuMemory.h) and dpu_push_xfer scatter/gather.
+//   PimData + DPU element-wise kernels (PimData.h:46-305, dpu/element-wise/*.c)
+//     -> ofhe_hip_mod{mul,add,sub}_vv / ofhe_hip_modmul_scalar.
+//   ChineseRemainderTransformFTTNat static tables (transformnat-impl.h:708-763)
+//     -> ofhe_plan_s, device-resident twiddles per (q, N).
+// No CPU fallback: every compute entry point launches HIP kernels or fails.
+#include <hip/hip_runtime.h>
+
+#include <atomic>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <new>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../../include/ofhe_hip.h"
+#include "eltwise_kernels.hpp"
+
+using namespace ofhe;
+typedef unsigned __int128 u128;
+
+#define OFHE_VERSION "ofhe-hip 0.1 gfx950"
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+    g_err = msg;
+    return code;
+}
+
+#define HIPCHK(call)                                                                        \
+    do {                                                                                    \
+        hipError_t e_ = (call);                                                             \
+        if (e_ != hipSuccess)                                                               \
+            return fail(OFHE_ERR_HIP, std::string(#call) + ": " + hipGetErrorString(e_));  \
+    } while (0)
+
+// ---- host-side number theory for table construction (setup, not timed) ----
+u64 mulmod(u64 a, u64 b, u64 q) { return (u64)(((u128)a * b) % q); }
+u64 powmod(u64 b, u64 e, u64 q) {
+    u64 r = 1 % q;
+    b %= q;
+    while (e) {
+        if (e & 1) r = mulmod(r, b, q);
+        b = mulmod(b, b, q);
+        e >>= 1;
+    }
+    return r;
+}
+u64 invmod(u64 a, u64 q) { return powmod(a, q - 2, q); }  // q prime
+u64 shoup_pre(u64 w, u64 q) { return (u64)(((u128)w << 64) / q); }
+unsigned msb64(u64 x) { return x ? 64u - (unsigned)__builtin_clzll(x) : 0u; }
+u32 bitrev(u32 x, unsigned bits) {
+    u32 r = 0;
+    for (unsigned i = 0; i < bits; i++) {
+        r = (r << 1) | (x & 1);
+        x >>= 1;
+    }
+    return r;
+}
+
+}  // namespace
+
+struct ofhe_ctx_s {
+    int device = 0;
+    std::atomic<int> live{1};
+};
+
+struct ofhe_plan_s {
+    ofhe_ctx_t ctx = nullptr;
+    u32 log_n = 0, towers = 0;
+    // device
+    TowerConst* d_tc = nullptr;
+    u64* d_tw = nullptr;
+    u64* d_itw = nullptr;
+    u64* d_itwn = nullptr;
+    // host copies (for ofhe_hip_plan_tables and scalar prep)
+    std::vector<u64> q, tab, tab_pre, itab, itab_pre, ninv;
+    u64* d_scal = nullptr;  // scratch for per-tower scalars (modmul_scalar)
+    std::mutex scal_mu;
+};
+
+struct ofhe_bconv_s {
+    ofhe_ctx_t ctx = nullptr;
+    BconvArgs args{};
+    u64* d_mem = nullptr;
+};
+
+// Entry points keep the C linkage of their declarations in include/ofhe_hip.h.
+const char* ofhe_hip_last_error(void) { return g_err.c_str(); }
+const char* ofhe_hip_version(void) { return OFHE_VERSION; }
+
+int ofhe_hip_device_count(int* count) {
+    if (!count) return fail(OFHE_ERR_ARG, "count is NULL");
+    HIPCHK(hipGetDeviceCount(count));
+    return OFHE_OK;
+}
+
+int ofhe_hip_init(int device, ofhe_ctx_t* ctx) {
+    if (!ctx) return fail(OFHE_ERR_ARG, "ctx is NULL");
+    int n = 0;
+    HIPCHK(hipGetDeviceCount(&n));
+    if (device < 0 || device >= n) return fail(OFHE_ERR_ARG, "device index out of range");
+    HIPCHK(hipSetDevice(device));
+    ofhe_ctx_s* c = new (std::nothrow) ofhe_ctx_s();
+    if (!c) return fail(OFHE_ERR_NOMEM, "context allocation failed");
+    c->device = device;
+    *ctx = c;
+    return OFHE_OK;
+}
+
+int ofhe_hip_finalize(ofhe_ctx_t ctx) {
+    if (!ctx) return fail(OFHE_ERR_ARG, "ctx is NULL");
+    if (ctx->live.exchange(0) == 0) return fail(OFHE_ERR_STATE, "context already finalized");
+    (void)hipSetDevice(ctx->device);
+    (void)hipDeviceSynchronize();
+    delete ctx;
+    return OFHE_OK;
+}
+
+int ofhe_hip_alloc(ofhe_ctx_t ctx, size_t bytes, void** dptr) {
+    if (!ctx || !dptr) return fail(OFHE_ERR_ARG, "NULL argument");
+    HIPCHK(hipSetDevice(ctx->device));
+    hipError_t e = hipMalloc(dptr, bytes ? bytes : 1);
+    if (e != hipSuccess) return fail(OFHE_ERR_NOMEM, std::string("hipMalloc: ") + hipGetErrorString(e));
+    return OFHE_OK;
+}
+
+int ofhe_hip_free(ofhe_ctx_t ctx, void* dptr) {
+    if (!ctx) return fail(OFHE_ERR_ARG, "ctx is NULL");
+    HIPCHK(hipSetDevice(ctx->device));
+    HIPCHK(hipFree(dptr));
+    return OFHE_OK;
+}
+
+// NULL selects the device's default (null) stream, as the header documents;
+// callers that want overlap pass their own stream (e.g. torch's).
+static hipStream_t pick(ofhe_ctx_t, void* stream) { return (hipStream_t)stream; }
+
+int ofhe_hip_copy_to_device(ofhe_ctx_t ctx, void* dst, const void* src, size_t bytes, void* stream) {
+    if (!ctx || (!dst && bytes) || (!src && bytes)) return fail(OFHE_ERR_ARG, "NULL argument");
+    HIPCHK(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, pick(ctx, stream)));
+    return OFHE_OK;
+}
+
+int ofhe_hip_copy_to_host(ofhe_ctx_t ctx, void* dst, const void* src, size_t bytes, void* stream) {
+    if (!ctx || (!dst && bytes) || (!src && bytes)) return fail(OFHE_ERR_ARG, "NULL argument");
+    HIPCHK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, pick(ctx, stream)));
+    return OFHE_OK;
+}
+
+int ofhe_hip_copy_device(ofhe_ctx_t ctx, void* dst, const void* src, size_t bytes, void* stream) {
+    if (!ctx || (!dst && bytes) || (!src && bytes)) return fail(OFHE_ERR_ARG, "NULL argument");
+    HIPCHK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, pick(ctx, stream)));
+    return OFHE_OK;
+}
+
+int ofhe_hip_sync(ofhe_ctx_t ctx, void* stream) {
+    if (!ctx) return fail(OFHE_ERR_ARG, "ctx is NULL");
+    HIPCHK(hipStreamSynchronize(pick(ctx, stream)));
+    return OFHE_OK;
+}
+
+// ---------------------------------------------------------------------------
+// Plans
+// ---------------------------------------------------------------------------
+int ofhe_hip_plan_create(ofhe_ctx_t ctx, uint32_t log_n, uint32_t towers, const uint64_t* q,
+                         const uint64_t* psi, ofhe_plan_t* plan) {
+    if (!ctx || !q || !psi || !plan) return fail(OFHE_ERR_ARG, "NULL argument");
+    if (log_n < 1 || log_n > 17) return fail(OFHE_ERR_ARG, "log_n must be in [1, 17]");
+    if (towers < 1 || towers > 4096) return fail(OFHE_ERR_ARG, "towers must be in [1, 4096]");
+    const u32 N = 1u << log_n;
+    const u64 m = 2ull * N;
+    for (u32 t = 0; t < towers; t++) {
+        if (q[t] < 3 || q[t] >= (1ull << 60) || !(q[t] & 1))
+            return fail(OFHE_ERR_ARG, "modulus " + std::to_string(t) + " must be odd and in [3, 2^60)");
+        if ((q[t] - 1) % m)
+            return fail(OFHE_ERR_ARG, "modulus " + std::to_string(t) + " is not 1 mod 2N");
+        if (psi[t] < 2 || psi[t] >= q[t] || powmod(psi[t], N, q[t]) != q[t] - 1)
+            return fail(OFHE_ERR_ARG, "root " + std::to_string(t) + " is not a primitive 2N-th root of unity");
+    }
+    ofhe_plan_s* p = new (std::nothrow) ofhe_plan_s();
+    if (!p) return fail(OFHE_ERR_NOMEM, "plan allocation failed");
+    p->ctx = ctx;
+    p->log_n = log_n;
+    p->towers = towers;
+    const size_t TN = (size_t)towers * N;
+    p->q.assign(q, q + towers);
+    p->tab.resize(TN);
+    p->tab_pre.resize(TN);
+    p->itab.resize(TN);
+    p->itab_pre.resize(TN);
+    p->ninv.resize(towers);
+    std::vector<TowerConst> tc(towers);
+    std::vector<u64> tw(2 * TN), itw(2 * TN), itwn(TN);
+    // PreCompute (transformnat-impl.h:708-763), one host thread per tower group
+    auto build = [&](u32 t) {
+        const u64 qt = q[t], ps = psi[t], psinv = invmod(ps, qt);
+        u64* T = &p->tab[(size_t)t * N];
+        u64* TI = &p->itab[(size_t)t * N];
+        u64 x = 1, xi = 1;
+        for (u32 i = 0; i < N; i++) {
+            const u32 r = bitrev(i, log_n);
+            T[r] = x;
+            TI[r] = xi;
+            x = mulmod(x, ps, qt);
+            xi = mulmod(xi, psinv, qt);
+        }
+        const u64 ni = invmod(N % qt, qt);
+        p->ninv[t] = ni;
+        for (u32 i = 0; i < N; i++) {
+            const size_t k = (size_t)t * N + i;
+            p->tab_pre[k] = shoup_pre(T[i], qt);
+            p->itab_pre[k] = shoup_pre(TI[i], qt);
+            tw[2 * k] = T[i];
+            tw[2 * k + 1] = p->tab_pre[k];
+            itw[2 * k] = TI[i];
+            itw[2 * k + 1] = p->itab_pre[k];
+        }
+        for (u32 i = 0; i < N / 2; i++) {
+            const u64 w = mulmod(TI[N / 2 + i], ni, qt);
+            itwn[(size_t)t * N + 2 * i] = w;
+            itwn[(size_t)t * N + 2 * i + 1] = shoup_pre(w, qt);
+        }
+        TowerConst c{};
+        c.q = qt;
+        c.ninv = ni;
+        c.ninv_pre = shoup_pre(ni, qt);
+        const unsigned mb = msb64(qt);
+        c.mu = (u64)((((u128)1) << (2 * mb + 3)) / qt);  // ComputeMu, ubintnat.h:651-656
+        c.nshift = mb - 2;
+        tc[t] = c;
+    };
+    {
+        unsigned nth = std::thread::hardware_concurrency();
+        if (nth < 1) nth = 1;
+        if (nth > towers) nth = towers;
+        if (nth > 16) nth = 16;
+        std::vector<std::thread> th;
+        for (unsigned w = 0; w < nth; w++)
+            th.emplace_back([&, w] {
+                for (u32 t = w; t < towers; t += nth) build(t);
+            });
+        for (auto& x : th) x.join();
+    }
+    hipError_t e = hipSetDevice(ctx->device);
+    if (e == hipSuccess) e = hipMalloc(&p->d_tc, sizeof(TowerConst) * towers);
+    if (e == hipSuccess) e = hipMalloc(&p->d_tw, sizeof(u64) * 2 * TN);
+    if (e == hipSuccess) e = hipMalloc(&p->d_itw, sizeof(u64) * 2 * TN);
+    if (e == hipSuccess) e = hipMalloc(&p->d_itwn, sizeof(u64) * TN);
+    if (e == hipSuccess) e = hipMalloc(&p->d_scal, sizeof(u64) * 2 * towers);
+    if (e == hipSuccess) e = hipMemcpy(p->d_tc, tc.data(), sizeof(TowerConst) * towers, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(p->d_tw, tw.data(), sizeof(u64) * 2 * TN, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(p->d_itw, itw.data(), sizeof(u64) * 2 * TN, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(p->d_itwn, itwn.data(), sizeof(u64) * TN, hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+        ofhe_hip_plan_destroy(p);
+        return fail(OFHE_ERR_HIP, std::string("plan upload: ") + hipGetErrorString(e));
+    }
+    *plan = p;
+    return OFHE_OK;
+}
+
+int ofhe_hip_plan_destroy(ofhe_plan_t p) {
+    if (!p) return fail(OFHE_ERR_ARG, "plan is NULL");
+    if (p->ctx) (void)hipSetDevice(p->ctx->device);
+    (void)hipFree(p->d_tc);
+    (void)hipFree(p->d_tw);
+    (void)hipFree(p->d_itw);
+    (void)hipFree(p->d_itwn);
+    (void)hipFree(p->d_scal);
+    delete p;
+    return OFHE_OK;
+}
+
+int ofhe_hip_plan_tables(ofhe_plan_t p, uint64_t* tab, uint64_t* tab_pre, uint64_t* itab,
+                         uint64_t* itab_pre, uint64_t* ninv) {
+    if (!p) return fail(OFHE_ERR_ARG, "plan is NULL");
+    const size_t n = p->tab.size() * sizeof(u64);
+    if (tab) memcpy(tab, p->tab.data(), n);
+    if (tab_pre) memcpy(tab_pre, p->tab_pre.data(), n);
+    if (itab) memcpy(itab, p->itab.data(), n);
+    if (itab_pre) memcpy(itab_pre, p->itab_pre.data(), n);
+    if (ninv) memcpy(ninv, p->ninv.data(), p->ninv.size() * sizeof(u64));
+    return OFHE_OK;
+}
+
+// ---------------------------------------------------------------------------
+// Launch helpers
+// ---------------------------------------------------------------------------
+static PlanArgs args_of(ofhe_plan_t p) {
+    PlanArgs a;
+    a.tc = p->d_tc;
+    a.tw = p->d_tw;
+    a.itw = p->d_itw;
+    a.itwn = p->d_itwn;
+    a.log_n = p->log_n;
+    a.towers = p->towers;
+    return a;
+}
+
+static int check_common(ofhe_plan_t p, uint32_t batch) {
+    if (!p || !p->ctx) return fail(OFHE_ERR_STATE, "plan is NULL or destroyed");
+    if (batch == 0) return fail(OFHE_ERR_ARG, "batch must be >= 1");
+    const u64 polys = (u64)batch * p->towers;
+    if (polys * ((u64)1 << p->log_n) / 4096 >= (1ull << 31))
+        return fail(OFHE_ERR_ARG, "batch too large for one launch");
+    return OFHE_OK;
+}
+
+template <int KA, bool INV>
+static void launch_cols_t(const PlanArgs& a, const u64* src, u64* dst, u32 batch, hipStream_t s) {
+    const u32 nwg = batch * a.towers * 16;
+    hipLaunchKernelGGL((k_cols<KA, INV>), dim3(nwg), dim3(256), 0, s, a, src, dst, batch, nwg);
+}
+
+static void launch_cols(const PlanArgs& a, bool inv, const u64* src, u64* dst, u32 batch, hipStream_t s) {
+    switch (a.log_n - 12) {
+#define CASE(K)                                               \
+    case K:                                                   \
+        if (inv)                                              \
+            launch_cols_t<K, true>(a, src, dst, batch, s);    \
+        else                                                  \
+            launch_cols_t<K, false>(a, src, dst, batch, s);   \
+        break;
+        CASE(1) CASE(2) CASE(3) CASE(4) CASE(5)
+#undef CASE
+        default: break;
+    }
+}
+
+template <int MODE>
+static void launch_block(const PlanArgs& a, const u64* src, u64* dst, const u64* b, u32 batch, hipStream_t s) {
+    const u32 nwg = batch * a.towers * (1u << (a.log_n - 12));
+    hipLaunchKernelGGL((k_block<MODE>), dim3(nwg), dim3(256), 0, s, a, src, dst, b, batch, nwg);
+}
+
+template <int MODE>
+static void launch_small(const PlanArgs& a, const u64* src, u64* dst, const u64* b, u32 batch, hipStream_t s) {
+    const u32 N = 1u << a.log_n;
+    const u32 thr = N / 2 >= 256 ? 256 : (N / 2 < 64 ? 64 : N / 2);
+    hipLaunchKernelGGL((k_small<MODE>), dim3(batch * a.towers), dim3(thr), 0, s, a, src, dst, b, batch);
+}
+
+static int post_launch() {
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return fail(OFHE_ERR_HIP, std::string("kernel launch: ") + hipGetErrorString(e));
+    return OFHE_OK;
+}
+
+int ofhe_hip_ntt_fwd(ofhe_plan_t p, uint64_t* data, uint32_t batch, void* stream) {
+    int rc = check_common(p, batch);
+    if (rc) return rc;
+    if (!data) return fail(OFHE_ERR_ARG, "data is NULL");
+    HIPCHK(hipSetDevice(p->ctx->device));
+    const PlanArgs a = args_of(p);
+    hipStream_t s = pick(p->ctx, stream);
+    if (p->log_n < 12) {
+        launch_small<MODE_FWD>(a, data, data, nullptr, batch, s);
+    } else {
+        if (p->log_n > 12) launch_cols(a, false, data, data, batch, s);
+        launch_block<MODE_FWD>(a, data, data, nullptr, batch, s);
+    }
+    return post_launch();
+}
+
+int ofhe_hip_ntt_inv(ofhe_plan_t p, uint64_t* data, uint32_t batch, void* stream) {
+    int rc = check_common(p, batch);
+    if (rc) return rc;
+    if (!data) return fail(OFHE_ERR_ARG, "data is NULL");
+    HIPCHK(hipSetDevice(p->ctx->device));
+    const PlanArgs a = args_of(p);
+    hipStream_t s = pick(p->ctx, stream);
+    if (p->log_n < 12) {
+        launch_small<MODE_INV>(a, data, data, nullptr, batch, s);
+    } else {
+        launch_block<MODE_INV>(a, data, data, nullptr, batch, s);
+        if (p->log_n > 12) launch_cols(a, true, data, data, batch, s);
+    }
+    return post_launch();
+}
+
+int ofhe_hip_ntt_mul_intt(ofhe_plan_t p, const uint64_t* a_, const uint64_t* b, uint64_t* c,
+                          uint32_t batch, void* stream) {
+    int rc = check_common(p, batch);
+    if (rc) return rc;
+    if (!a_ || !b || !c) return fail(OFHE_ERR_ARG, "NULL data pointer");
+    if (b == c && a_ != c) return fail(OFHE_ERR_ARG, "c may alias a but not b");
+    HIPCHK(hipSetDevice(p->ctx->device));
+    const PlanArgs a = args_of(p);
+    hipStream_t s = pick(p->ctx, stream);
+    if (p->log_n < 12) {
+        launch_small<MODE_FUSED>(a, a_, c, b, batch, s);
+    } else if (p->log_n == 12) {
+        launch_block<MODE_FUSED>(a, a_, c, b, batch, s);
+    } else {
+        launch_cols(a, false, a_, c, batch, s);
+        launch_block<MODE_FUSED>(a, c, c, b, batch, s);
+        launch_cols(a, true, c, c, batch, s);
+    }
+    return post_launch();
+}
+
+int ofhe_hip_ntt_mul_intt_stage(ofhe_plan_t p, int stage, const uint64_t* a_, const uint64_t* b, uint64_t* c,
+                                uint32_t batch, void* stream) {
+    int rc = check_common(p, batch);
+    if (rc) return rc;
+    if (!a_ || !b || !c) return fail(OFHE_ERR_ARG, "NULL data pointer");
+    if (stage < 0 || stage > 2) return fail(OFHE_ERR_ARG, "stage must be 0, 1 or 2");
+    HIPCHK(hipSetDevice(p->ctx->device));
+    const PlanArgs a = args_of(p);
+    hipStream_t s = pick(p->ctx, stream);
+    if (p->log_n < 12) {
+        if (stage == 1) launch_small<MODE_FUSED>(a, a_, c, b, batch, s);
+    } else if (p->log_n == 12) {
+        if (stage == 1) launch_block<MODE_FUSED>(a, a_, c, b, batch, s);
+    } else if (stage == 0) {
+        launch_cols(a, false, a_, c, batch, s);
+    } else if (stage == 1) {
+        launch_block<MODE_FUSED>(a, c, c, b, batch, s);
+    } else {
+        launch_cols(a, true, c, c, batch, s);
+    }
+    return post_launch();
+}
+
+template <int OP>
+static int eltwise(ofhe_plan_t p, const u64* a, const u64* b, u64* c, u32 batch, void* stream) {
+    int rc = check_common(p, batch);
+    if (rc) return rc;
+    if (!a || !b || !c) return fail(OFHE_ERR_ARG, "NULL data pointer");
+    HIPCHK(hipSetDevice(p->ctx->device));
+    const u64 npairs = (u64)batch * p->towers * ((u64)1 << p->log_n) / 2;
+    u64 blocks = (npairs + 255) / 256;
+    if (blocks > 256 * 16) blocks = 256 * 16;
+    hipLaunchKernelGGL((k_eltwise<OP>), dim3((u32)blocks), dim3(256), 0, pick(p->ctx, stream), p->d_tc, a, b,
+                       c, npairs, p->log_n, p->towers);
+    return post_launch();
+}
+
+int ofhe_hip_modmul_vv(ofhe_plan_t p, const uint64_t* a, const uint64_t* b, uint64_t* c, uint32_t batch,
+                       void* stream) {
+    return eltwise<ELT_MUL>(p, a, b, c, batch, stream);
+}
+int ofhe_hip_modadd_vv(ofhe_plan_t p, const uint64_t* a, const uint64_t* b, uint64_t* c, uint32_t batch,
+                       void* stream) {
+    return eltwise<ELT_ADD>(p, a, b, c, batch, stream);
+}
+int ofhe_hip_modsub_vv(ofhe_plan_t p, const uint64_t* a, const uint64_t* b, uint64_t* c, uint32_t batch,
+                       void* stream) {
+    return eltwise<ELT_SUB>(p, a, b, c, batch, stream);
+}
+
+int ofhe_hip_modmul_scalar(ofhe_plan_t p, const uint64_t* a, const uint64_t* s, uint64_t* c,
+                           uint32_t batch, void* stream) {
+    int rc = check_common(p, batch);
+    if (rc) return rc;
+    if (!s) return fail(OFHE_ERR_ARG, "scalar array is NULL");
+    // ModMul(const IntegerType&) reduces the scalar first, then Shoup
+    // (mubintvecnat.cpp:310-332).
+    std::vector<u64> sp(2 * p->towers);
+    for (u32 t = 0; t < p->towers; t++) {
+        const u64 v = s[t] % p->q[t];
+        sp[2 * t] = v;
+        sp[2 * t + 1] = shoup_pre(v, p->q[t]);
+    }
+    // the scalar table is tiny; it rides on the same stream, serialised by
+    // the plan's mutex so concurrent callers on one plan do not race on it.
+    std::lock_guard<std::mutex> lk(p->scal_mu);
+    HIPCHK(hipSetDevice(p->ctx->device));
+    hipStream_t st = pick(p->ctx, stream);
+    HIPCHK(hipMemcpyAsync(p->d_scal, sp.data(), sizeof(u64) * sp.size(), hipMemcpyHostToDevice, st));
+    HIPCHK(hipStreamSynchronize(st));
+    return eltwise<ELT_MULS>(p, a, p->d_scal, c, batch, stream);
+}
+
+// ---------------------------------------------------------------------------
+// Base conversion
+// ---------------------------------------------------------------------------
+int ofhe_hip_bconv_create(ofhe_ctx_t ctx, uint32_t log_n, uint32_t size_q, uint32_t size_p,
+                          const uint64_t* q, const uint64_t* p, const uint64_t* qhat_inv_modq,
+                          const uint64_t* qhat_modp, ofhe_bconv_t* out) {
+    if (!ctx || !q || !p || !qhat_inv_modq || !qhat_modp || !out) return fail(OFHE_ERR_ARG, "NULL argument");
+    if (log_n < 1 || log_n > 17) return fail(OFHE_ERR_ARG, "log_n must be in [1, 17]");
+    if (size_q < 1 || size_p < 1 || size_q > 256 || size_p > 256)
+        return fail(OFHE_ERR_ARG, "size_q and size_p must be in [1, 256]");
+    for (u32 i = 0; i < size_q; i++)
+        if (q[i] < 2 || q[i] >= (1ull << 60)) return fail(OFHE_ERR_ARG, "q out of range");
+    for (u32 j = 0; j < size_p; j++)
+        if (p[j] < 2 || p[j] >= (1ull << 60)) return fail(OFHE_ERR_ARG, "p out of range");
+    // layout: qv[Q] | qhinv[2Q] | qhmodp[Q*P] | pv[P] | pmu[2P]
+    const size_t words = size_q + 2 * size_q + (size_t)size_q * size_p + size_p + 2 * size_p;
+    std::vector<u64> h(words);
+    u64* qv = h.data();
+    u64* qhinv = qv + size_q;
+    u64* qhmodp = qhinv + 2 * size_q;
+    u64* pv = qhmodp + (size_t)size_q * size_p;
+    u64* pmu = pv + size_p;
+    for (u32 i = 0; i < size_q; i++) {
+        qv[i] = q[i];
+        qhinv[2 * i] = qhat_inv_modq[i] % q[i];
+        qhinv[2 * i + 1] = shoup_pre(qhinv[2 * i], q[i]);
+    }
+    memcpy(qhmodp, qhat_modp, sizeof(u64) * size_q * size_p);
+    for (u32 j = 0; j < size_p; j++) {
+        pv[j] = p[j];
+        const u128 mu = (~(u128)0) / p[j];  // floor(2^128 / p), p odd
+        pmu[2 * j] = (u64)mu;
+        pmu[2 * j + 1] = (u64)(mu >> 64);
+    }
+    ofhe_bconv_s* b = new (std::nothrow) ofhe_bconv_s();
+    if (!b) return fail(OFHE_ERR_NOMEM, "bconv allocation failed");
+    b->ctx = ctx;
+    hipError_t e = hipSetDevice(ctx->device);
+    if (e == hipSuccess) e = hipMalloc(&b->d_mem, words * sizeof(u64));
+    if (e == hipSuccess) e = hipMemcpy(b->d_mem, h.data(), words * sizeof(u64), hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+        (void)hipFree(b->d_mem);
+        delete b;
+        return fail(OFHE_ERR_HIP, std::string("bconv upload: ") + hipGetErrorString(e));
+    }
+    BconvArgs& A = b->args;
+    A.qv = b->d_mem;
+    A.qhinv = A.qv + size_q;
+    A.qhmodp = A.qhinv + 2 * size_q;
+    A.pv = A.qhmodp + (size_t)size_q * size_p;
+    A.pmu = A.pv + size_p;
+    A.log_n = log_n;
+    A.size_q = size_q;
+    A.size_p = size_p;
+    *out = b;
+    return OFHE_OK;
+}
+
+int ofhe_hip_bconv_destroy(ofhe_bconv_t b) {
+    if (!b) return fail(OFHE_ERR_ARG, "bconv is NULL");
+    if (b->ctx) (void)hipSetDevice(b->ctx->device);
+    (void)hipFree(b->d_mem);
+    delete b;
+    return OFHE_OK;
+}
+
+int ofhe_hip_approx_switch_crt_basis(ofhe_bconv_t b, const uint64_t* x, uint64_t* out, uint32_t batch,
+                                     void* stream) {
+    if (!b || !b->ctx) return fail(OFHE_ERR_STATE, "bconv is NULL or destroyed");
+    if (!x || !out || batch == 0) return fail(OFHE_ERR_ARG, "bad data argument");
+    HIPCHK(hipSetDevice(b->ctx->device));
+    const u64 total = (u64)batch << b->args.log_n;
+    const u64 blocks = (total + 255) / 256;
+    if (blocks >= (1ull << 31)) return fail(OFHE_ERR_ARG, "batch too large");
+    hipLaunchKernelGGL((k_bconv<8>), dim3((u32)blocks), dim3(256), 0, pick(b->ctx, stream), b->args, x, out,
+                       batch);
+    return post_launch();
+}
+

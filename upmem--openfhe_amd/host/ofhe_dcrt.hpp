@@ -1,0 +1,329 @@
+// ofhe_dcrt.hpp -- C++ host side of the gfx950 backend, above the C ABI.
+//
+// Mirrors the reference's interfaces for the hot path so OpenFHE-side code
+// (and these tests) read the same way:
+//   HipManager::getHip(dev)   <- PimManager::getPim(nr_dpus, profile)
+//                                (src/core/include/pim/PimManager.h:23-29,44-85)
+//   DeviceBuffer              <- PimData's device allocation (PimData.h:16-34, RAII)
+//   DCRTPolyHip               <- DCRTPolyImpl's operator surface used by the
+//                                schemes (lattice/hal/default/dcrtpoly.h:142-200,
+//                                dcrtpoly-impl.h:410-416, 1034-1063, 2518-2524):
+//                                SwitchFormat/SetFormat, Plus/Minus/Times and the
+//                                in-place operators, scalar Times, ApproxSwitchCRTBasis.
+// Errors: any non-zero C-ABI status becomes ofhe::math_error, the analogue of
+// OPENFHE_THROW(math_error, ...) (src/core/include/utils/exception.h:162).
+// Device layout: a DCRTPolyHip of `batch` polynomials is one contiguous
+// [batch][towers][N] buffer -- towers are contiguous, unlike the reference's
+// std::vector<PolyImpl> (dcrtpoly.h:421), so one launch covers every tower.
+#pragma once
+
+#include <cstdint>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <stdexcept>
+#include <string>
+#include <utility>
+#include <vector>
+
+#include "../../include/ofhe_hip.h"
+
+namespace ofhe {
+
+class math_error : public std::runtime_error {
+public:
+    explicit math_error(const std::string& m) : std::runtime_error(m) {}
+};
+class not_implemented_error : public std::runtime_error {
+public:
+    explicit not_implemented_error(const std::string& m) : std::runtime_error(m) {}
+};
+
+inline void check(int rc, const char* what) {
+    if (rc != OFHE_OK) throw math_error(std::string(what) + ": " + ofhe_hip_last_error());
+}
+
+// ---------------------------------------------------------------------------
+// HipManager: lazily created per-device singleton, creation guarded by a
+// mutex (PimManager.h:23-29); owns the device context and its stream.
+// ---------------------------------------------------------------------------
+class HipManager {
+public:
+    static HipManager* getHip(int device = 0) {
+        static std::mutex mu;
+        static std::map<int, std::unique_ptr<HipManager>> inst;
+        std::lock_guard<std::mutex> lk(mu);
+        auto& p = inst[device];
+        if (!p) p.reset(new HipManager(device));
+        return p.get();
+    }
+    ofhe_ctx_t ctx() const { return ctx_; }
+    int device() const { return device_; }
+    void* allocate(size_t bytes) {
+        void* p = nullptr;
+        check(ofhe_hip_alloc(ctx_, bytes, &p), "HipManager::allocate");
+        return p;
+    }
+    void deallocate(void* p) { check(ofhe_hip_free(ctx_, p), "HipManager::deallocate"); }
+    void copy_to_device(void* dst, const void* src, size_t bytes) {
+        check(ofhe_hip_copy_to_device(ctx_, dst, src, bytes, nullptr), "HipManager::copy_to_device");
+    }
+    void copy_from_device(void* dst, const void* src, size_t bytes) {
+        check(ofhe_hip_copy_to_host(ctx_, dst, src, bytes, nullptr), "HipManager::copy_from_device");
+        sync();
+    }
+    void sync() { check(ofhe_hip_sync(ctx_, nullptr), "HipManager::sync"); }
+    ~HipManager() {
+        if (ctx_) ofhe_hip_finalize(ctx_);
+    }
+    HipManager(const HipManager&) = delete;
+    HipManager& operator=(const HipManager&) = delete;
+
+private:
+    explicit HipManager(int device) : device_(device) { check(ofhe_hip_init(device, &ctx_), "HipManager"); }
+    int device_;
+    ofhe_ctx_t ctx_ = nullptr;
+};
+
+// RAII device buffer of uint64 words.
+class DeviceBuffer {
+public:
+    DeviceBuffer() = default;
+    DeviceBuffer(HipManager* m, size_t words) : m_(m), n_(words) {
+        if (words) p_ = static_cast<uint64_t*>(m_->allocate(words * sizeof(uint64_t)));
+    }
+    DeviceBuffer(const DeviceBuffer&) = delete;
+    DeviceBuffer& operator=(const DeviceBuffer&) = delete;
+    DeviceBuffer(DeviceBuffer&& o) noexcept { swap(o); }
+    DeviceBuffer& operator=(DeviceBuffer&& o) noexcept {
+        swap(o);
+        return *this;
+    }
+    ~DeviceBuffer() {
+        if (p_) ofhe_hip_free(m_->ctx(), p_);
+    }
+    uint64_t* get() const { return p_; }
+    size_t size() const { return n_; }
+    void upload(const uint64_t* h) { m_->copy_to_device(p_, h, n_ * 8); }
+    void download(uint64_t* h) const { m_->copy_from_device(h, p_, n_ * 8); }
+    void copy_from(const DeviceBuffer& o) {
+        check(ofhe_hip_copy_device(m_->ctx(), p_, o.p_, n_ * 8, nullptr), "DeviceBuffer::copy_from");
+    }
+
+private:
+    void swap(DeviceBuffer& o) {
+        std::swap(m_, o.m_);
+        std::swap(p_, o.p_);
+        std::swap(n_, o.n_);
+    }
+    HipManager* m_ = nullptr;
+    uint64_t* p_ = nullptr;
+    size_t n_ = 0;
+};
+
+// ---------------------------------------------------------------------------
+// Parameters: (cyclotomic order, moduli, roots) as ILDCRTParams, with the NTT
+// plan cached per (N, moduli) -- the reference caches twiddles per modulus in
+// static maps (transformnat.h:352-368).
+// ---------------------------------------------------------------------------
+class DCRTParams {
+public:
+    DCRTParams(uint32_t cyclotomic_order, std::vector<uint64_t> moduli, std::vector<uint64_t> roots,
+               int device = 0)
+        : m_(cyclotomic_order), q_(std::move(moduli)), r_(std::move(roots)), mgr_(HipManager::getHip(device)) {
+        if (m_ < 4 || (m_ & (m_ - 1))) throw math_error("CyclotomicOrder is not a power of two");
+        if (q_.size() != r_.size() || q_.empty()) throw math_error("moduli/roots size mismatch");
+        uint32_t n = m_ / 2, lg = 0;
+        while ((1u << lg) < n) lg++;
+        log_n_ = lg;
+        check(ofhe_hip_plan_create(mgr_->ctx(), log_n_, (uint32_t)q_.size(), q_.data(), r_.data(), &plan_),
+              "DCRTParams: plan");
+    }
+    ~DCRTParams() {
+        if (plan_) ofhe_hip_plan_destroy(plan_);
+    }
+    DCRTParams(const DCRTParams&) = delete;
+    DCRTParams& operator=(const DCRTParams&) = delete;
+    uint32_t GetCyclotomicOrder() const { return m_; }
+    uint32_t GetRingDimension() const { return m_ / 2; }
+    uint32_t LogN() const { return log_n_; }
+    size_t Towers() const { return q_.size(); }
+    const std::vector<uint64_t>& Moduli() const { return q_; }
+    const std::vector<uint64_t>& Roots() const { return r_; }
+    ofhe_plan_t plan() const { return plan_; }
+    HipManager* manager() const { return mgr_; }
+
+private:
+    uint32_t m_, log_n_ = 0;
+    std::vector<uint64_t> q_, r_;
+    HipManager* mgr_;
+    ofhe_plan_t plan_ = nullptr;
+};
+
+enum class Format { EVALUATION = 0, COEFFICIENT = 1 };
+
+// ---------------------------------------------------------------------------
+// DCRTPolyHip: `batch` DCRT polynomials resident on one device.  With one
+// tower it is also the PimData op set (PimData.h:46-168: + - * and
+// ModAdd/ModSub/ModMul with vector or scalar right-hand sides).
+// ---------------------------------------------------------------------------
+class DCRTPolyHip {
+public:
+    DCRTPolyHip(std::shared_ptr<DCRTParams> p, Format f, uint32_t batch = 1)
+        : p_(std::move(p)), f_(f), batch_(batch),
+          buf_(p_->manager(), (size_t)batch * p_->Towers() * p_->GetRingDimension()) {
+        std::vector<uint64_t> z(buf_.size(), 0);
+        buf_.upload(z.data());
+    }
+    DCRTPolyHip(const DCRTPolyHip& o) : p_(o.p_), f_(o.f_), batch_(o.batch_), buf_(o.p_->manager(), o.buf_.size()) {
+        buf_.copy_from(o.buf_);
+    }
+    DCRTPolyHip(DCRTPolyHip&&) = default;
+    DCRTPolyHip& operator=(DCRTPolyHip&&) = default;
+
+    const std::shared_ptr<DCRTParams>& GetParams() const { return p_; }
+    Format GetFormat() const { return f_; }
+    uint32_t Batch() const { return batch_; }
+    uint64_t* data() const { return buf_.get(); }
+    size_t words() const { return buf_.size(); }
+
+    // values[b][t][i] flattened; must be canonical (< q_t)
+    void SetValues(const std::vector<uint64_t>& flat, Format f) {
+        if (flat.size() != buf_.size()) throw math_error("SetValues: size mismatch");
+        buf_.upload(flat.data());
+        f_ = f;
+    }
+    std::vector<uint64_t> GetValues() const {
+        std::vector<uint64_t> h(buf_.size());
+        buf_.download(h.data());
+        return h;
+    }
+    // tower t of batch entry b (GetElementAtIndex(t) analogue)
+    std::vector<uint64_t> GetElementAtIndex(size_t t, uint32_t b = 0) const {
+        auto all = GetValues();
+        const size_t n = p_->GetRingDimension();
+        const size_t off = ((size_t)b * p_->Towers() + t) * n;
+        return std::vector<uint64_t>(all.begin() + off, all.begin() + off + n);
+    }
+
+    // SwitchFormat (dcrtpoly-impl.h:2518-2524 -> poly-impl.h:412-432)
+    void SwitchFormat() {
+        if (f_ == Format::COEFFICIENT) {
+            check(ofhe_hip_ntt_fwd(p_->plan(), data(), batch_, nullptr), "SwitchFormat");
+            f_ = Format::EVALUATION;
+        } else {
+            check(ofhe_hip_ntt_inv(p_->plan(), data(), batch_, nullptr), "SwitchFormat");
+            f_ = Format::COEFFICIENT;
+        }
+    }
+    void SetFormat(Format f) {
+        if (f != f_) SwitchFormat();
+    }
+
+    DCRTPolyHip Plus(const DCRTPolyHip& rhs) const {
+        check_compat(rhs, "Plus", false);
+        DCRTPolyHip r(p_, f_, batch_);
+        check(ofhe_hip_modadd_vv(p_->plan(), data(), rhs.data(), r.data(), batch_, nullptr), "Plus");
+        return r;
+    }
+    DCRTPolyHip Minus(const DCRTPolyHip& rhs) const {
+        check_compat(rhs, "Minus", false);
+        DCRTPolyHip r(p_, f_, batch_);
+        check(ofhe_hip_modsub_vv(p_->plan(), data(), rhs.data(), r.data(), batch_, nullptr), "Minus");
+        return r;
+    }
+    // Times (dcrtpoly.h:185-200): EVALUATION format only
+    DCRTPolyHip Times(const DCRTPolyHip& rhs) const {
+        check_compat(rhs, "Times", true);
+        DCRTPolyHip r(p_, f_, batch_);
+        check(ofhe_hip_modmul_vv(p_->plan(), data(), rhs.data(), r.data(), batch_, nullptr), "Times");
+        return r;
+    }
+    // Times(const std::vector<NativeInteger>&): one scalar per tower (Shoup)
+    DCRTPolyHip Times(const std::vector<uint64_t>& scalars) const {
+        if (scalars.size() != p_->Towers()) throw math_error("Times: one scalar per tower required");
+        DCRTPolyHip r(p_, f_, batch_);
+        check(ofhe_hip_modmul_scalar(p_->plan(), data(), scalars.data(), r.data(), batch_, nullptr), "Times");
+        return r;
+    }
+    DCRTPolyHip& operator+=(const DCRTPolyHip& rhs) {
+        check_compat(rhs, "operator+=", false);
+        check(ofhe_hip_modadd_vv(p_->plan(), data(), rhs.data(), data(), batch_, nullptr), "operator+=");
+        return *this;
+    }
+    DCRTPolyHip& operator-=(const DCRTPolyHip& rhs) {
+        check_compat(rhs, "operator-=", false);
+        check(ofhe_hip_modsub_vv(p_->plan(), data(), rhs.data(), data(), batch_, nullptr), "operator-=");
+        return *this;
+    }
+    DCRTPolyHip& operator*=(const DCRTPolyHip& rhs) {
+        check_compat(rhs, "operator*=", true);
+        check(ofhe_hip_modmul_vv(p_->plan(), data(), rhs.data(), data(), batch_, nullptr), "operator*=");
+        return *this;
+    }
+    DCRTPolyHip operator+(const DCRTPolyHip& rhs) const { return Plus(rhs); }
+    DCRTPolyHip operator-(const DCRTPolyHip& rhs) const { return Minus(rhs); }
+    DCRTPolyHip operator*(const DCRTPolyHip& rhs) const { return Times(rhs); }
+
+    // c = INTT(NTT(this) (.) rhs): this in COEFFICIENT, rhs in EVALUATION; the
+    // result is COEFFICIENT.  Equal to SwitchFormat; *= rhs; SwitchFormat.
+    DCRTPolyHip MulViaNTT(const DCRTPolyHip& rhs) const {
+        if (f_ != Format::COEFFICIENT || rhs.f_ != Format::EVALUATION)
+            throw not_implemented_error("MulViaNTT: needs COEFFICIENT x EVALUATION");
+        check_compat(rhs, "MulViaNTT", false, false);
+        DCRTPolyHip r(p_, Format::COEFFICIENT, batch_);
+        check(ofhe_hip_ntt_mul_intt(p_->plan(), data(), rhs.data(), r.data(), batch_, nullptr), "MulViaNTT");
+        return r;
+    }
+
+    bool operator==(const DCRTPolyHip& o) const {
+        return f_ == o.f_ && p_->Moduli() == o.p_->Moduli() && GetValues() == o.GetValues();
+    }
+
+private:
+    void check_compat(const DCRTPolyHip& rhs, const char* op, bool eval_only, bool same_format = true) const {
+        if (p_->GetRingDimension() != rhs.p_->GetRingDimension())
+            throw math_error(std::string(op) + ": RingDimension missmatch");
+        if (same_format && f_ != rhs.f_) throw not_implemented_error(std::string(op) + ": Format missmatch");
+        if (eval_only && (f_ != Format::EVALUATION || rhs.f_ != Format::EVALUATION))
+            throw not_implemented_error(std::string(op) + " for DCRTPolyHip supported only in Format::EVALUATION");
+        if (p_->Towers() != rhs.p_->Towers()) throw math_error(std::string(op) + ": tower size mismatch");
+        if (p_->Moduli() != rhs.p_->Moduli()) throw math_error(std::string(op) + ": Modulus missmatch");
+        if (batch_ != rhs.batch_) throw math_error(std::string(op) + ": batch mismatch");
+    }
+
+    std::shared_ptr<DCRTParams> p_;
+    Format f_;
+    uint32_t batch_;
+    DeviceBuffer buf_;
+};
+
+// ---------------------------------------------------------------------------
+// ApproxSwitchCRTBasis (dcrtpoly-impl.h:1034-1063): x over basis Q (params of
+// x) -> basis P (paramsP), both COEFFICIENT form.
+// ---------------------------------------------------------------------------
+class BaseConverter {
+public:
+    BaseConverter(const DCRTParams& Q, const DCRTParams& P, const std::vector<uint64_t>& QHatInvModq,
+                  const std::vector<uint64_t>& QHatModp /* [sizeQ][sizeP] */) {
+        check(ofhe_hip_bconv_create(Q.manager()->ctx(), Q.LogN(), (uint32_t)Q.Towers(), (uint32_t)P.Towers(),
+                                    Q.Moduli().data(), P.Moduli().data(), QHatInvModq.data(), QHatModp.data(), &h_),
+              "BaseConverter");
+    }
+    ~BaseConverter() {
+        if (h_) ofhe_hip_bconv_destroy(h_);
+    }
+    BaseConverter(const BaseConverter&) = delete;
+    BaseConverter& operator=(const BaseConverter&) = delete;
+    DCRTPolyHip ApproxSwitchCRTBasis(const DCRTPolyHip& x, const std::shared_ptr<DCRTParams>& paramsP) const {
+        if (x.GetFormat() != Format::COEFFICIENT) throw math_error("ApproxSwitchCRTBasis: COEFFICIENT form expected");
+        DCRTPolyHip out(paramsP, Format::COEFFICIENT, x.Batch());
+        check(ofhe_hip_approx_switch_crt_basis(h_, x.data(), out.data(), x.Batch(), nullptr), "ApproxSwitchCRTBasis");
+        return out;
+    }
+
+private:
+    ofhe_bconv_t h_ = nullptr;
+};
+
+}  // namespace ofhe

@@ -1,0 +1,263 @@
+"""ctypes binding of the gfx950 RNS backend (C ABI: include/ofhe_hip.h).
+
+Host-side mirror of the reference's offload interface for the hot path:
+
+* ``Context``   ~ ``PimManager::getPim`` (src/core/include/pim/PimManager.h:23-29):
+  one per device, allocation and host<->device copies.
+* ``NTTPlan``   ~ ``ChineseRemainderTransformFTT<NativeVector>`` with its
+  ``PreCompute`` tables (transformnat-impl.h:575-763) plus the
+  ``NativeVectorT`` element-wise ops (mubintvecnat.cpp:245-367) over
+  [batch][tower][N] device buffers.
+* ``BaseConverter`` ~ ``DCRTPolyImpl::ApproxSwitchCRTBasis`` (dcrtpoly-impl.h:1034-1063).
+
+Errors raise ``MathError`` (the analogue of ``lbcrypto::math_error`` thrown by
+``OPENFHE_THROW``).  Pointers are plain integers (e.g. ``torch.Tensor.data_ptr()``)
+and streams are ``hipStream_t`` values as integers (``torch.cuda.Stream.cuda_stream``).
+
+There is no CPU fallback: if ``lib/libofhe_hip.so`` is missing this module
+raises on first use.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import Optional, Sequence
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libofhe_hip.so")
+
+_u64p = ctypes.POINTER(ctypes.c_uint64)
+_vp = ctypes.c_void_p
+
+
+class MathError(RuntimeError):
+    """Raised when a backend call returns a non-zero status (cf. lbcrypto::math_error)."""
+
+
+_lib: Optional[ctypes.CDLL] = None
+
+# name -> (restype, argtypes)
+_SIGS = {
+    "ofhe_hip_last_error": (ctypes.c_char_p, []),
+    "ofhe_hip_version": (ctypes.c_char_p, []),
+    "ofhe_hip_device_count": (ctypes.c_int, [ctypes.POINTER(ctypes.c_int)]),
+    "ofhe_hip_init": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(_vp)]),
+    "ofhe_hip_finalize": (ctypes.c_int, [_vp]),
+    "ofhe_hip_alloc": (ctypes.c_int, [_vp, ctypes.c_size_t, ctypes.POINTER(_vp)]),
+    "ofhe_hip_free": (ctypes.c_int, [_vp, _vp]),
+    "ofhe_hip_copy_to_device": (ctypes.c_int, [_vp, _vp, _vp, ctypes.c_size_t, _vp]),
+    "ofhe_hip_copy_to_host": (ctypes.c_int, [_vp, _vp, _vp, ctypes.c_size_t, _vp]),
+    "ofhe_hip_copy_device": (ctypes.c_int, [_vp, _vp, _vp, ctypes.c_size_t, _vp]),
+    "ofhe_hip_sync": (ctypes.c_int, [_vp, _vp]),
+    "ofhe_hip_plan_create": (ctypes.c_int, [_vp, ctypes.c_uint32, ctypes.c_uint32, _u64p, _u64p,
+                                            ctypes.POINTER(_vp)]),
+    "ofhe_hip_plan_destroy": (ctypes.c_int, [_vp]),
+    "ofhe_hip_plan_tables": (ctypes.c_int, [_vp, _u64p, _u64p, _u64p, _u64p, _u64p]),
+    "ofhe_hip_ntt_fwd": (ctypes.c_int, [_vp, _vp, ctypes.c_uint32, _vp]),
+    "ofhe_hip_ntt_inv": (ctypes.c_int, [_vp, _vp, ctypes.c_uint32, _vp]),
+    "ofhe_hip_modmul_vv": (ctypes.c_int, [_vp, _vp, _vp, _vp, ctypes.c_uint32, _vp]),
+    "ofhe_hip_modadd_vv": (ctypes.c_int, [_vp, _vp, _vp, _vp, ctypes.c_uint32, _vp]),
+    "ofhe_hip_modsub_vv": (ctypes.c_int, [_vp, _vp, _vp, _vp, ctypes.c_uint32, _vp]),
+    "ofhe_hip_modmul_scalar": (ctypes.c_int, [_vp, _vp, _u64p, _vp, ctypes.c_uint32, _vp]),
+    "ofhe_hip_ntt_mul_intt": (ctypes.c_int, [_vp, _vp, _vp, _vp, ctypes.c_uint32, _vp]),
+    "ofhe_hip_ntt_mul_intt_stage": (ctypes.c_int, [_vp, ctypes.c_int, _vp, _vp, _vp, ctypes.c_uint32, _vp]),
+    "ofhe_hip_bconv_create": (ctypes.c_int, [_vp, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
+                                             _u64p, _u64p, _u64p, _u64p, ctypes.POINTER(_vp)]),
+    "ofhe_hip_bconv_destroy": (ctypes.c_int, [_vp]),
+    "ofhe_hip_approx_switch_crt_basis": (ctypes.c_int, [_vp, _vp, _vp, ctypes.c_uint32, _vp]),
+}
+
+EXPORTED_SYMBOLS = tuple(_SIGS)
+
+
+def lib() -> ctypes.CDLL:
+    """Load (once) and return the backend library; raise if it is not built."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise MathError(
+                f"HIP backend not built: {LIB_PATH} is missing "
+                "(run __graft_entry__.build() or make -C upmem--openfhe_amd/csrc)")
+        L = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in _SIGS.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def _check(rc: int) -> None:
+    if rc != 0:
+        msg = lib().ofhe_hip_last_error().decode(errors="replace")
+        raise MathError(f"ofhe_hip error {rc}: {msg}")
+
+
+def _arr(vals: Sequence[int]):
+    return (ctypes.c_uint64 * len(vals))(*[int(v) for v in vals])
+
+
+def version() -> str:
+    return lib().ofhe_hip_version().decode()
+
+
+def device_count() -> int:
+    n = ctypes.c_int(0)
+    _check(lib().ofhe_hip_device_count(ctypes.byref(n)))
+    return n.value
+
+
+class Context:
+    """Per-device context (PimManager analogue)."""
+
+    def __init__(self, device: int = 0):
+        h = _vp()
+        _check(lib().ofhe_hip_init(int(device), ctypes.byref(h)))
+        self._h = h
+        self.device = device
+
+    @property
+    def handle(self):
+        if self._h is None:
+            raise MathError("context finalized")
+        return self._h
+
+    def close(self) -> None:
+        if self._h is not None:
+            _check(lib().ofhe_hip_finalize(self._h))
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def alloc(self, nbytes: int) -> int:
+        p = _vp()
+        _check(lib().ofhe_hip_alloc(self.handle, int(nbytes), ctypes.byref(p)))
+        return p.value
+
+    def free(self, ptr: int) -> None:
+        _check(lib().ofhe_hip_free(self.handle, _vp(ptr)))
+
+    def copy_to_device(self, dst: int, src: int, nbytes: int, stream: int = 0) -> None:
+        _check(lib().ofhe_hip_copy_to_device(self.handle, _vp(dst), _vp(src), int(nbytes), _vp(stream or None)))
+
+    def copy_to_host(self, dst: int, src: int, nbytes: int, stream: int = 0) -> None:
+        _check(lib().ofhe_hip_copy_to_host(self.handle, _vp(dst), _vp(src), int(nbytes), _vp(stream or None)))
+
+    def copy_device(self, dst: int, src: int, nbytes: int, stream: int = 0) -> None:
+        _check(lib().ofhe_hip_copy_device(self.handle, _vp(dst), _vp(src), int(nbytes), _vp(stream or None)))
+
+    def sync(self, stream: int = 0) -> None:
+        _check(lib().ofhe_hip_sync(self.handle, _vp(stream or None)))
+
+
+class NTTPlan:
+    """Device-resident NTT tables for N = 2**log_n and one modulus per tower.
+
+    Data buffers are [batch][towers][N] uint64 residues in device memory.
+    """
+
+    def __init__(self, ctx: Context, log_n: int, moduli: Sequence[int], roots: Sequence[int]):
+        if len(moduli) != len(roots):
+            raise MathError("moduli and roots differ in length")
+        self.ctx = ctx
+        self.log_n = int(log_n)
+        self.n = 1 << self.log_n
+        self.moduli = [int(q) for q in moduli]
+        self.roots = [int(r) for r in roots]
+        self.towers = len(self.moduli)
+        h = _vp()
+        _check(lib().ofhe_hip_plan_create(ctx.handle, self.log_n, self.towers, _arr(self.moduli),
+                                          _arr(self.roots), ctypes.byref(h)))
+        self._h = h
+
+    @property
+    def handle(self):
+        if self._h is None:
+            raise MathError("plan destroyed")
+        return self._h
+
+    def close(self) -> None:
+        if self._h is not None:
+            _check(lib().ofhe_hip_plan_destroy(self._h))
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def tables(self):
+        """Host copies of (Table, TableP, TableI, TableIP, ninv) as flat lists."""
+        tn = self.towers * self.n
+        a, b, c, d = (ctypes.c_uint64 * tn)(), (ctypes.c_uint64 * tn)(), (ctypes.c_uint64 * tn)(), (ctypes.c_uint64 * tn)()
+        e = (ctypes.c_uint64 * self.towers)()
+        _check(lib().ofhe_hip_plan_tables(self.handle, a, b, c, d, e))
+        return list(a), list(b), list(c), list(d), list(e)
+
+    # --- transforms (ChineseRemainderTransformFTT) ---
+    def forward(self, data: int, batch: int = 1, stream: int = 0) -> None:
+        _check(lib().ofhe_hip_ntt_fwd(self.handle, _vp(data), int(batch), _vp(stream or None)))
+
+    def inverse(self, data: int, batch: int = 1, stream: int = 0) -> None:
+        _check(lib().ofhe_hip_ntt_inv(self.handle, _vp(data), int(batch), _vp(stream or None)))
+
+    # --- NativeVectorT element-wise (vector, vector) ---
+    def mod_mul(self, a: int, b: int, c: int, batch: int = 1, stream: int = 0) -> None:
+        _check(lib().ofhe_hip_modmul_vv(self.handle, _vp(a), _vp(b), _vp(c), int(batch), _vp(stream or None)))
+
+    def mod_add(self, a: int, b: int, c: int, batch: int = 1, stream: int = 0) -> None:
+        _check(lib().ofhe_hip_modadd_vv(self.handle, _vp(a), _vp(b), _vp(c), int(batch), _vp(stream or None)))
+
+    def mod_sub(self, a: int, b: int, c: int, batch: int = 1, stream: int = 0) -> None:
+        _check(lib().ofhe_hip_modsub_vv(self.handle, _vp(a), _vp(b), _vp(c), int(batch), _vp(stream or None)))
+
+    def mod_mul_scalar(self, a: int, scalars: Sequence[int], c: int, batch: int = 1, stream: int = 0) -> None:
+        if len(scalars) != self.towers:
+            raise MathError("one scalar per tower required")
+        _check(lib().ofhe_hip_modmul_scalar(self.handle, _vp(a), _arr(scalars), _vp(c), int(batch),
+                                            _vp(stream or None)))
+
+    # --- the metric pipeline ---
+    def ntt_mul_intt(self, a: int, b: int, c: int, batch: int = 1, stream: int = 0) -> None:
+        _check(lib().ofhe_hip_ntt_mul_intt(self.handle, _vp(a), _vp(b), _vp(c), int(batch), _vp(stream or None)))
+
+
+    def ntt_mul_intt_stage(self, stage: int, a: int, b: int, c: int, batch: int = 1, stream: int = 0) -> None:
+        """One kernel of ntt_mul_intt (0: forward columns, 1: fused block pass, 2: inverse columns)."""
+        _check(lib().ofhe_hip_ntt_mul_intt_stage(self.handle, int(stage), _vp(a), _vp(b), _vp(c), int(batch),
+                                                 _vp(stream or None)))
+
+
+class BaseConverter:
+    """ApproxSwitchCRTBasis from basis Q (size_q towers) to basis P (size_p towers)."""
+
+    def __init__(self, ctx: Context, log_n: int, q: Sequence[int], p: Sequence[int],
+                 qhat_inv_modq: Sequence[int], qhat_modp: Sequence[int]):
+        self.ctx = ctx
+        self.log_n = int(log_n)
+        self.size_q, self.size_p = len(q), len(p)
+        if len(qhat_inv_modq) != self.size_q or len(qhat_modp) != self.size_q * self.size_p:
+            raise MathError("precomputation sizes do not match the bases")
+        h = _vp()
+        _check(lib().ofhe_hip_bconv_create(ctx.handle, self.log_n, self.size_q, self.size_p, _arr(q), _arr(p),
+                                           _arr(qhat_inv_modq), _arr(qhat_modp), ctypes.byref(h)))
+        self._h = h
+
+    def close(self) -> None:
+        if self._h is not None:
+            _check(lib().ofhe_hip_bconv_destroy(self._h))
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def switch(self, x: int, out: int, batch: int = 1, stream: int = 0) -> None:
+        _check(lib().ofhe_hip_approx_switch_crt_basis(self._h, _vp(x), _vp(out), int(batch), _vp(stream or None)))
