@@ -79,6 +79,12 @@ int ofhe_hip_sync(ofhe_ctx_t ctx, void* stream);
 int ofhe_hip_plan_create(ofhe_ctx_t ctx, uint32_t log_n, uint32_t towers, const uint64_t* q,
                          const uint64_t* psi, ofhe_plan_t* plan);
 int ofhe_hip_plan_destroy(ofhe_plan_t plan);
+/* Performance knob for ofhe_hip_ntt_mul_intt at log_n > 12: process the batch
+ * in chunks of `chunk_batch` entries (0 = whole batch in one pass) and, with
+ * streams = 2, alternate the chunks over two internal streams forked from and
+ * joined back into the caller's stream.  Results are identical for any
+ * setting; only speed changes. */
+int ofhe_hip_plan_tune(ofhe_plan_t plan, uint32_t chunk_batch, uint32_t streams);
 /* Copy the plan's host-side tables out (debug / parity tests): any pointer
  * may be NULL.  tab*: [towers][N] in OpenFHE order (Table[rev(i)] = psi^i). */
 int ofhe_hip_plan_tables(ofhe_plan_t plan, uint64_t* tab, uint64_t* tab_pre, uint64_t* itab,

@@ -270,3 +270,57 @@ def test_errors_raise(hip, O):
         plan.forward(0, 1, stream())                   # NULL data
     with pytest.raises(H.MathError):
         plan.forward(1 << 20, 0, stream())             # empty batch
+
+
+def _generic_moduli(O, log_n, towers, bits=58):
+    """NTT primes q = 1 mod 2N in the middle of [2^bits, 2^(bits+1)): NOT of the
+    special form 2^L - d (d < 2^32), so the generic Shoup kernels run."""
+    m = 2 << log_n
+    qs, rs = [], []
+    cand = ((3 << (bits - 1)) // m) * m + 1  # ~1.5 * 2^bits
+    while len(qs) < towers:
+        if O.lib().oracle_is_prime(cand):
+            qs.append(cand)
+            rs.append(O.root_of_unity(m, cand))
+        cand += m
+    return qs, rs
+
+
+@pytest.mark.parametrize("log_n,towers,batch", [(11, 2, 2), (12, 2, 2), (13, 3, 1), (16, 2, 2), (17, 1, 1)])
+def test_generic_moduli_vs_oracle(hip, O, log_n, towers, batch):
+    """Moduli that are not 2^L - d: exercises the generic (non special-prime) kernels."""
+    H, ctx = hip
+    n = 1 << log_n
+    qs, rs = _generic_moduli(O, log_n, towers)
+    assert all((q >> 32) != (1 << (q.bit_length() - 32)) - 1 for q in qs)
+    tb = O.Tables(n, qs, rs)
+    a = O.uniform_dcrt(batch, towers, n, qs, 300 + log_n)
+    b = O.uniform_dcrt(batch, towers, n, qs, 400 + log_n)
+    got = run_all_ops(H, H.NTTPlan(ctx, log_n, qs, rs), a, b)
+    assert np.array_equal(got["ntt_a"], O.ntt_fwd(a, tb))
+    assert np.array_equal(got["intt_a"], O.ntt_inv(a, tb))
+    assert np.array_equal(got["pipeline"], O.ntt_mul_intt(a, b, tb))
+
+
+def test_special_prime_switch_identical(hip, O, monkeypatch):
+    """Special-prime and generic kernels give identical results on the same
+    (special-form) moduli; OFHE_NO_SPQ forces the generic instantiation."""
+    import torch
+
+    H, ctx = hip
+    log_n, T, B = 16, 4, 2
+    n = 1 << log_n
+    qs, rs = O.moduli_chain(log_n, T)
+    a = O.uniform_dcrt(B, T, n, qs, 5)
+    b = O.uniform_dcrt(B, T, n, qs, 6)
+    outs = []
+    for env in (None, "1"):
+        if env:
+            monkeypatch.setenv("OFHE_NO_SPQ", env)
+        plan = H.NTTPlan(ctx, log_n, qs, rs)
+        xa, xb = dev(a), dev(b)
+        xc = torch.empty_like(xa)
+        plan.ntt_mul_intt(xa.data_ptr(), xb.data_ptr(), xc.data_ptr(), B, stream())
+        outs.append(host(xc))
+    assert np.array_equal(outs[0], outs[1])
+    assert np.array_equal(outs[0], O.ntt_mul_intt(a, b, O.Tables(n, qs, rs)))

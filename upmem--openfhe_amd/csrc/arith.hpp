@@ -1,19 +1,24 @@
 // arith.hpp -- 64-bit modular arithmetic for gfx950 (device side).
 //
-// gfx950 has no 64x64 multiplier: every u64 product is built from the
-// quarter-rate v_mad_u64_u32 / v_mul_lo_u32 / v_mul_hi_u32 (measured
-// ~18 T lane-ops/s each vs ~70 T for full-rate VALU, tools/microbench).
-// The NTT is therefore VALU(multiply)-bound, and these helpers are written
-// to minimise multiplies:
-//   * mulhi_approx: floor(a*b/2^64) - {0,1} with 3 mads (drops the a0*b0
-//     carry, Harvey-style slack absorbed by lazy reduction);
-//   * shoup_lazy: a*w mod q in [0, 3q) (Shoup / Harvey, "FASTER ARITHMETIC FOR
-//     NUMBER-THEORETIC TRANSFORMS"; reference: ubintnat.h:1478-1497 computes
-//     the canonical form);
+// gfx950 has no 64x64 integer multiplier: a u64 product is built from
+// v_mad_u64_u32 / v_mul_lo_u32 / v_mul_hi_u32, each a multi-cycle VALU op
+// (tools/microbench/*.hip; the block kernel runs at ~100 % of the VALU issue
+// capacity by SQ counters, profiles/).  The NTT is therefore bound by integer
+// multiplies, and these helpers minimise them:
+//   * mulhi_approx: floor(a*b/2^64) - {0,1,2} with 3 multiplies (drops the
+//     a0*b0 term and one carry; lazy reduction absorbs the slack);
+//   * shoup_lazy: a*w mod q in [0, 4q) (Shoup/Harvey, "Faster arithmetic for
+//     number-theoretic transforms"; the reference's canonical form is
+//     NativeIntegerT::ModMulFastConstEq, ubintnat.h:1491-1497) -- 9 multiplies,
+//     8 when q = 2^L - d with d < 2^32 (Mod<true>, see below);
 //   * barrett_ref: bit-exact restatement of NativeIntegerT::ModMulFastEq
-//     (ubintnat.h:1399-1413), used for the vector x vector Hadamard product.
+//     (ubintnat.h:1399-1413) for the vector x vector Hadamard product.
 // All moduli satisfy q < 2^60 (OpenFHE MAX_MODULUS_SIZE = 60, basicint.h:44),
 // so lazy values up to 8q < 2^63 never overflow.
+//
+// Alternatives measured and rejected (tools/exp_variants.py):
+// VCC-free sign-mask conditional subtract, add_co/addc-chained 64-bit adds,
+// splitting the fused multiply-adds into v_mul_lo_u32 + adds.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -25,16 +30,19 @@ typedef uint32_t u32;
 
 __device__ __forceinline__ u32 lo32(u64 x) { return (u32)x; }
 __device__ __forceinline__ u32 hi32(u64 x) { return (u32)(x >> 32); }
+__device__ __forceinline__ u64 pack(u32 lo, u32 hi) { return ((u64)hi << 32) | lo; }
 
 // v_mad_u64_u32: a*b + c, exact in 64 bits for 32-bit a, b, c < 2^64 - (2^32-1)^2
 __device__ __forceinline__ u64 mad32(u32 a, u32 b, u64 c) { return (u64)a * (u64)b + c; }
 
-// floor(a*b / 2^64) or one less.  3 x v_mad_u64_u32 + one 64-bit add.
+__device__ __forceinline__ u64 csub(u64 x, u64 m) { return x >= m ? x - m : x; }
+
+// floor(a*b / 2^64) - e, e in {0, 1, 2}: drops a0*b0 and the carry of the
+// middle sum.
 __device__ __forceinline__ u64 mulhi_approx(u64 a, u64 b) {
-    u64 m1 = mad32(lo32(a), hi32(b), 0);
-    u64 m2 = mad32(hi32(a), lo32(b), (u64)lo32(m1));
-    u64 h = mad32(hi32(a), hi32(b), (u64)hi32(m1));
-    return h + (u64)hi32(m2);
+    const u64 m1 = mad32(lo32(a), hi32(b), 0);
+    const u64 m2 = mad32(hi32(a), lo32(b), 0);
+    return mad32(hi32(a), hi32(b), (m1 >> 32) + (m2 >> 32));
 }
 
 // exact floor(a*b / 2^64)
@@ -46,20 +54,42 @@ __device__ __forceinline__ u64 mulhi_exact(u64 a, u64 b) {
     return h + (u64)hi32(m2);
 }
 
-// low 64 bits of a*b: 1 mad + 2 mul_lo (folded into mads by the compiler)
-__device__ __forceinline__ u64 mullo(u64 a, u64 b) { return a * b; }
+// Modulus constants for the lazy butterflies.  SPQ ("special prime") marks a
+// modulus q = 2^L - d with 33 <= L <= 60 and d < 2^32, i.e. hi32(q) is all
+// ones below bit L-32.  Then 2^64 - q has high word 2^32 - 2^(L-32), and the
+// cross product lo32(qh) * hi32(2^64-q) is -(lo32(qh) << (L-32)): a shift
+// instead of a multiply.  Every modulus chain OpenFHE builds with
+// FirstPrime/PreviousPrime near 2^L (nbtheory-impl.h:334-379) has this form.
+template <bool SPQ>
+struct Mod {
+    u64 q;    // modulus, q < 2^60
+    u64 q4;   // 4q
+    u64 nq;   // 2^64 - q   (loaded, not derived, so LLVM keeps the adds)
+    u64 nq4;  // 2^64 - 4q
+    u32 sh;   // L - 32 (SPQ only)
+};
 
-// Shoup with precomputed wp = floor(w*2^64/q): a*w mod q in [0, 3q) for any a < 2^64.
-__device__ __forceinline__ u64 shoup_lazy(u64 a, u64 w, u64 wp, u64 q) {
-    u64 qh = mulhi_approx(a, wp);
-    return a * w - qh * q;
+// Shoup with precomputed wp = floor(w*2^64/q): a*w mod q in [0, 4q) for any
+// a < 2^64.  Harvey's bound gives [0, 2q) with the exact quotient; the
+// approximate quotient is at most 2 short.  The remainder is formed as
+// lo64(a*w) + lo64(qh*(2^64-q)), so there is no 64-bit subtraction.
+template <bool SPQ>
+__device__ __forceinline__ u64 shoup_lazy(u64 a, u64 w, u64 wp, const Mod<SPQ>& M) {
+    const u64 qh = mulhi_approx(a, wp);
+    u64 s = mad32(lo32(a), lo32(w), 0);
+    s = mad32(lo32(qh), lo32(M.nq), s);
+    u32 hi;
+    if (SPQ)
+        hi = hi32(s) + lo32(a) * hi32(w) + hi32(a) * lo32(w) - (lo32(qh) << M.sh) + hi32(qh) * lo32(M.nq);
+    else
+        hi = hi32(s) + lo32(a) * hi32(w) + hi32(a) * lo32(w) + lo32(qh) * hi32(M.nq) + hi32(qh) * lo32(M.nq);
+    return pack(lo32(s), hi);
 }
 
-__device__ __forceinline__ u64 csub(u64 x, u64 m) { return x >= m ? x - m : x; }
-
-// canonical Shoup: ModMulFastConstEq semantics (result in [0, q)).
+// canonical Shoup: ModMulFastConstEq semantics (result in [0, q)), generic q.
 __device__ __forceinline__ u64 shoup_canon(u64 a, u64 w, u64 wp, u64 q) {
-    u64 r = shoup_lazy(a, w, wp, q);
+    const Mod<false> M{q, 4 * q, 0 - q, 0 - 4 * q, 0};
+    u64 r = shoup_lazy(a, w, wp, M);
     r = csub(r, 2 * q);
     return csub(r, q);
 }

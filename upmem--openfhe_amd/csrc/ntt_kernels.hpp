@@ -13,16 +13,17 @@
 //
 // Decomposition for N = 2^logN >= 2^12 (one tower = 512 KiB at 2^16, more
 // than a CU's 160 KiB LDS):
-//   k_cols  : the first logN-12 stages. Each thread owns one "column"
+//   k_cols  : the first logN-12 stages. Each thread owns one or two "columns"
 //             {c + 4096 k}; all its butterflies are in registers.
-//   k_block : the last 12 stages on contiguous 4096-element blocks (32 KiB of
+//   k_block : the last 12 stages on contiguous 4096-element blocks (34 KiB of
 //             LDS per workgroup): 3 rounds of 4 radix-2 stages held in
-//             registers (16 values per thread), two XOR-swizzled LDS
-//             exchanges between rounds (bank-conflict free for all three
-//             access patterns, checked by tools/lds_banks.py).
+//             registers (16 values per thread), two padded LDS exchanges
+//             between rounds (see lds_pad()).
 //   The metric pipeline runs k_cols(fwd) -> k_block(fwd + Hadamard + inverse)
 //   -> k_cols(inv): the Hadamard and the 24 block stages share one residency.
 // N <= 2^11 uses k_small (whole tower in LDS, one stage per step).
+// Every kernel is instantiated for generic moduli (SPQ = false) and for
+// moduli q = 2^L - d, d < 2^32 (SPQ = true, one fewer multiply per Shoup).
 #pragma once
 #include "arith.hpp"
 
@@ -33,9 +34,15 @@ struct TowerConst {
     u64 ninv;      // N^-1 mod q
     u64 ninv_pre;  // Shoup precon of ninv
     u64 mu;        // ComputeMu() for Barrett (ubintnat.h:651-656)
+    u64 nq;        // 2^64 - q   (loaded, not derived: keeps LLVM from turning
+    u64 nq4;       // 2^64 - 4q   the lazy adds back into carry-chain subtractions)
     u32 nshift;    // msb(q) - 2
-    u32 pad;
+    u32 spq_sh;    // msb(q) - 32 when q = 2^msb - d with d < 2^32, else 0
 };
+template <bool SPQ>
+__device__ __forceinline__ Mod<SPQ> load_mod(const TowerConst& tc) {
+    return Mod<SPQ>{tc.q, 4 * tc.q, tc.nq, tc.nq4, tc.spq_sh};
+}
 
 // Device view of a plan. Twiddles are interleaved (w, w') pairs so one
 // 16-byte load fetches a twiddle and its Shoup precon.
@@ -51,8 +58,7 @@ struct PlanArgs {
 enum { MODE_FWD = 0, MODE_INV = 1, MODE_FUSED = 2 };
 
 // Bijective XCD-aware block remap (cdna_hip_programming.md T1): consecutive
-// work items land on the same XCD, so workgroups of one tower share its
-// twiddles in that XCD's L2.
+// work items land on the same XCD.
 __device__ __forceinline__ u32 xcd_remap(u32 bid, u32 nwg) {
     u32 q = nwg >> 3, r = nwg & 7, xcd = bid & 7, loc = bid >> 3;
     return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + loc;
@@ -66,29 +72,31 @@ __device__ __forceinline__ Tw ldtw(const u64* base, u32 idx) {
     return Tw{v.x, v.y};
 }
 
-// Cooley-Tukey butterfly, inputs in [0, 8q), outputs in [0, 7q).
-__device__ __forceinline__ void ct_bfly(u64& x, u64& y, Tw w, u64 q, u64 q3, u64 q4) {
-    u64 t = shoup_lazy(y, w.w, w.wp, q);  // [0, 3q)
-    u64 a = csub(x, q4);                  // [0, 4q)
+// Cooley-Tukey butterfly, inputs in [0, 8q), outputs in [0, 8q).
+template <class M_>
+__device__ __forceinline__ void ct_bfly(u64& x, u64& y, Tw w, const M_& M) {
+    const u64 t = shoup_lazy(y, w.w, w.wp, M);  // [0, 4q)
+    const u64 a = csub(x, M.q4);                // [0, 4q)
     x = a + t;
-    y = a + (q3 - t);
+    y = a + M.q4 - t;
 }
 
 // Gentleman-Sande butterfly, inputs in [0, 4q), outputs in [0, 4q).
-__device__ __forceinline__ void gs_bfly(u64& x, u64& y, Tw w, u64 q, u64 q4) {
-    u64 s = x + y;                                    // [0, 8q)
-    u64 d = x + (q4 - y);                             // (0, 8q)
-    x = csub(s, q4);
-    y = shoup_lazy(d, w.w, w.wp, q);                  // [0, 3q)
+template <class M_>
+__device__ __forceinline__ void gs_bfly(u64& x, u64& y, Tw w, const M_& M) {
+    const u64 s = x + y;          // [0, 8q)
+    const u64 d = x + M.q4 - y;   // (0, 8q)
+    x = csub(s, M.q4);
+    y = shoup_lazy(d, w.w, w.wp, M);  // [0, 4q)
 }
 
 // First inverse stage (t = 1) with N^-1 folded in: both outputs scaled.
-__device__ __forceinline__ void gs_bfly_ninv(u64& x, u64& y, Tw wn, u64 ninv, u64 ninv_pre, u64 q,
-                                             u64 q4) {
-    u64 s = x + y;
-    u64 d = x + (q4 - y);
-    x = shoup_lazy(s, ninv, ninv_pre, q);
-    y = shoup_lazy(d, wn.w, wn.wp, q);
+template <class M_>
+__device__ __forceinline__ void gs_bfly_ninv(u64& x, u64& y, Tw wn, u64 ninv, u64 ninv_pre, const M_& M) {
+    const u64 s = x + y;
+    const u64 d = x + M.q4 - y;
+    x = shoup_lazy(s, ninv, ninv_pre, M);
+    y = shoup_lazy(d, wn.w, wn.wp, M);
 }
 
 __device__ __forceinline__ u64 canon8(u64 x, u64 q) {  // [0, 8q) -> [0, q)
@@ -107,51 +115,78 @@ __device__ __forceinline__ u64 canon4(u64 x, u64 q) {  // [0, 4q) -> [0, q)
 // (k, k + 2^(3-s)); its twiddle index is 2^s * M0 + (k >> (4 - s)) with
 // M0 = N/(16 st) + (global index of the 16*st super-group).
 // ---------------------------------------------------------------------------
-template <int S>
-__device__ __forceinline__ void fwd_stage16(u64 (&v)[16], const u64* tw, u32 M0, u64 q, u64 q3,
-                                            u64 q4) {
+template <int S, class M_>
+__device__ __forceinline__ void fwd_stage16(u64 (&v)[16], const u64* tw, u32 M0, const M_& M) {
     constexpr int half = 8 >> S;
+    const u64* base = tw + 2 * ((u64)M0 << S);  // one address per stage, j as immediate offsets
 #pragma unroll
     for (int j = 0; j < (1 << S); j++) {
-        Tw w = ldtw(tw, (M0 << S) + j);
+        Tw w = ldtw(base, j);
 #pragma unroll
-        for (int k = j * 2 * half; k < j * 2 * half + half; k++) ct_bfly(v[k], v[k + half], w, q, q3, q4);
+        for (int k = j * 2 * half; k < j * 2 * half + half; k++) ct_bfly(v[k], v[k + half], w, M);
     }
 }
 
-template <int S>
-__device__ __forceinline__ void inv_stage16(u64 (&v)[16], const u64* itw, u32 M0, u64 q, u64 q4) {
+template <int S, class M_>
+__device__ __forceinline__ void inv_stage16(u64 (&v)[16], const u64* itw, u32 M0, const M_& M) {
     constexpr int half = 8 >> S;
+    const u64* base = itw + 2 * ((u64)M0 << S);
 #pragma unroll
     for (int j = 0; j < (1 << S); j++) {
-        Tw w = ldtw(itw, (M0 << S) + j);
+        Tw w = ldtw(base, j);
 #pragma unroll
-        for (int k = j * 2 * half; k < j * 2 * half + half; k++) gs_bfly(v[k], v[k + half], w, q, q4);
+        for (int k = j * 2 * half; k < j * 2 * half + half; k++) gs_bfly(v[k], v[k + half], w, M);
     }
 }
 
 // last inverse round stage s = 3 at global t = 1: uses the N^-1-folded table.
 // itwn is indexed by i = (M0 << 3) + j - N/2.
-__device__ __forceinline__ void inv_stage16_first(u64 (&v)[16], const u64* itwn, u32 i0,
-                                                  const TowerConst& tc, u64 q4) {
+template <class M_>
+__device__ __forceinline__ void inv_stage16_first(u64 (&v)[16], const u64* itwn, u32 i0, const TowerConst& tc,
+                                                  const M_& M) {
+    const u64* base = itwn + 2 * (u64)i0;
 #pragma unroll
     for (int j = 0; j < 8; j++) {
-        Tw w = ldtw(itwn, i0 + j);
-        gs_bfly_ninv(v[2 * j], v[2 * j + 1], w, tc.ninv, tc.ninv_pre, tc.q, q4);
+        Tw w = ldtw(base, j);
+        gs_bfly_ninv(v[2 * j], v[2 * j + 1], w, tc.ninv, tc.ninv_pre, M);
     }
 }
 
-__device__ __forceinline__ u32 swz(u32 p) { return p ^ ((p >> 4) & 15u) ^ (((p >> 8) & 15u) << 4); }
+template <class M_>
+__device__ __forceinline__ void fwd_round16(u64 (&v)[16], const u64* tw, u32 M0, const M_& M) {
+    fwd_stage16<0>(v, tw, M0, M);
+    fwd_stage16<1>(v, tw, M0, M);
+    fwd_stage16<2>(v, tw, M0, M);
+    fwd_stage16<3>(v, tw, M0, M);
+}
+template <class M_>
+__device__ __forceinline__ void inv_round16(u64 (&v)[16], const u64* itw, u32 M0, const M_& M) {
+    inv_stage16<3>(v, itw, M0, M);
+    inv_stage16<2>(v, itw, M0, M);
+    inv_stage16<1>(v, itw, M0, M);
+    inv_stage16<0>(v, itw, M0, M);
+}
+
+// LDS placement of block element p: one u64 of padding per 16 elements.  It is
+// additive, so every round addresses its 16 values as one base register plus
+// immediate offsets, and it is bank-conflict free for the round-2/3 patterns
+// and 2-way on one half-wave for round 1 (tools/lds_banks.py).
+__device__ __forceinline__ u32 lds_pad(u32 p) { return p + (p >> 4); }
+constexpr u32 LDS_WORDS = 4096 + 4096 / 16;
 
 // ---------------------------------------------------------------------------
 // k_block: the last 12 stages on a 4096-element block; MODE selects
 // forward (canonical out), inverse (first 12 inverse stages), or the fused
 // forward -> Hadamard -> inverse pipeline.
 // ---------------------------------------------------------------------------
-template <int MODE>
-__global__ __launch_bounds__(256) void k_block(PlanArgs P, const u64* src, u64* dst,
-                                               const u64* __restrict__ bdat, u32 batch, u32 nwg) {
-    __shared__ u64 lds[4096];
+#ifndef OFHE_KB_WAVES
+#define OFHE_KB_WAVES 4
+#endif
+template <int MODE, bool SPQ, int NR>
+__global__ __launch_bounds__(256, OFHE_KB_WAVES) void k_block(PlanArgs P, const u64* src, u64* dst,
+                                                              const u64* __restrict__ bdat, u32 batch, u32 nwg) {
+    static_assert(NR == 2 || NR == 3, "k_block covers the last 8 (NR=2) or 12 (NR=3) stages");
+    __shared__ u64 lds[LDS_WORDS];
     const u32 tid = threadIdx.x;
     const u32 logn = P.log_n;
     const u32 N = 1u << logn;
@@ -164,50 +199,42 @@ __global__ __launch_bounds__(256) void k_block(PlanArgs P, const u64* src, u64* 
     const u64* blk = src + off;
     u64* oblk = dst + off;
     const TowerConst tc = P.tc[t];
-    const u64 q = tc.q, q3 = 3 * q, q4 = 4 * q;
+    const u64 q = tc.q;
+    const Mod<SPQ> M = load_mod<SPQ>(tc);
     const u64* tw = P.tw + (u64)t * N * 2;
     const u64* itw = P.itw + (u64)t * N * 2;
     const u64* itwn = P.itwn + (u64)t * N;  // N/2 pairs
     const u32 h = tid >> 4, r = tid & 15;
+    // padded LDS bases (lds_pad(p) = p + p/16) of the three round layouts
+    const u32 L1 = tid + h;      // lds_pad(tid + 256 k)      = L1 + 272 k
+    const u32 L2 = h * 272 + r;  // lds_pad(256 h + r + 16 k) = L2 + 17 k
+    const u32 L3 = tid * 17;     // lds_pad(16 tid + k)       = L3 + k
     u64 v[16];
 
     if (MODE == MODE_FWD || MODE == MODE_FUSED) {
-        // round 1: st = 256, p = tid + 256k
+        if (NR == 3) {
+            // round 1: st = 256, p = tid + 256k
 #pragma unroll
-        for (int k = 0; k < 16; k++) v[k] = blk[tid + 256 * k];
-        {
-            const u32 M0 = (N >> 12) + g;
-            fwd_stage16<0>(v, tw, M0, q, q3, q4);
-            fwd_stage16<1>(v, tw, M0, q, q3, q4);
-            fwd_stage16<2>(v, tw, M0, q, q3, q4);
-            fwd_stage16<3>(v, tw, M0, q, q3, q4);
+            for (int k = 0; k < 16; k++) v[k] = blk[tid + 256 * k];
+            fwd_round16(v, tw, (N >> 12) + g, M);
+#pragma unroll
+            for (int k = 0; k < 16; k++) lds[L1 + 272 * k] = v[k];
+            __syncthreads();
+            // round 2: st = 16, p = h*256 + r + 16k
+#pragma unroll
+            for (int k = 0; k < 16; k++) v[k] = lds[L2 + 17 * k];
+        } else {
+#pragma unroll
+            for (int k = 0; k < 16; k++) v[k] = blk[h * 256 + r + 16 * k];
         }
+        fwd_round16(v, tw, (N >> 8) + g * 16 + h, M);
 #pragma unroll
-        for (int k = 0; k < 16; k++) lds[swz(tid + 256 * k)] = v[k];
-        __syncthreads();
-        // round 2: st = 16, p = h*256 + r + 16k
-#pragma unroll
-        for (int k = 0; k < 16; k++) v[k] = lds[swz(h * 256 + r + 16 * k)];
-        {
-            const u32 M0 = (N >> 8) + g * 16 + h;
-            fwd_stage16<0>(v, tw, M0, q, q3, q4);
-            fwd_stage16<1>(v, tw, M0, q, q3, q4);
-            fwd_stage16<2>(v, tw, M0, q, q3, q4);
-            fwd_stage16<3>(v, tw, M0, q, q3, q4);
-        }
-#pragma unroll
-        for (int k = 0; k < 16; k++) lds[swz(h * 256 + r + 16 * k)] = v[k];
+        for (int k = 0; k < 16; k++) lds[L2 + 17 * k] = v[k];
         __syncthreads();
         // round 3: st = 1, p = 16 tid + k
 #pragma unroll
-        for (int k = 0; k < 16; k++) v[k] = lds[swz(tid * 16 + k)];
-        {
-            const u32 M0 = (N >> 4) + g * 256 + tid;
-            fwd_stage16<0>(v, tw, M0, q, q3, q4);
-            fwd_stage16<1>(v, tw, M0, q, q3, q4);
-            fwd_stage16<2>(v, tw, M0, q, q3, q4);
-            fwd_stage16<3>(v, tw, M0, q, q3, q4);
-        }
+        for (int k = 0; k < 16; k++) v[k] = lds[L3 + k];
+        fwd_round16(v, tw, (N >> 4) + g * 256 + tid, M);
 #pragma unroll
         for (int k = 0; k < 16; k++) v[k] = canon8(v[k], q);
         if (MODE == MODE_FWD) {
@@ -237,35 +264,28 @@ __global__ __launch_bounds__(256) void k_block(PlanArgs P, const u64* src, u64* 
     // inverse round 3': st = 1, GS stages t = 1, 2, 4, 8 (s = 3, 2, 1, 0)
     {
         const u32 M0 = (N >> 4) + g * 256 + tid;
-        inv_stage16_first(v, itwn, (M0 << 3) - (N >> 1), tc, q4);
-        inv_stage16<2>(v, itw, M0, q, q4);
-        inv_stage16<1>(v, itw, M0, q, q4);
-        inv_stage16<0>(v, itw, M0, q, q4);
+        inv_stage16_first(v, itwn, (M0 << 3) - (N >> 1), tc, M);
+        inv_stage16<2>(v, itw, M0, M);
+        inv_stage16<1>(v, itw, M0, M);
+        inv_stage16<0>(v, itw, M0, M);
     }
 #pragma unroll
-    for (int k = 0; k < 16; k++) lds[swz(tid * 16 + k)] = v[k];
+    for (int k = 0; k < 16; k++) lds[L3 + k] = v[k];
     __syncthreads();
 #pragma unroll
-    for (int k = 0; k < 16; k++) v[k] = lds[swz(h * 256 + r + 16 * k)];
-    {
-        const u32 M0 = (N >> 8) + g * 16 + h;
-        inv_stage16<3>(v, itw, M0, q, q4);
-        inv_stage16<2>(v, itw, M0, q, q4);
-        inv_stage16<1>(v, itw, M0, q, q4);
-        inv_stage16<0>(v, itw, M0, q, q4);
+    for (int k = 0; k < 16; k++) v[k] = lds[L2 + 17 * k];
+    inv_round16(v, itw, (N >> 8) + g * 16 + h, M);
+    if (NR == 2) {
+#pragma unroll
+        for (int k = 0; k < 16; k++) oblk[h * 256 + r + 16 * k] = v[k];
+        return;
     }
 #pragma unroll
-    for (int k = 0; k < 16; k++) lds[swz(h * 256 + r + 16 * k)] = v[k];
+    for (int k = 0; k < 16; k++) lds[L2 + 17 * k] = v[k];
     __syncthreads();
 #pragma unroll
-    for (int k = 0; k < 16; k++) v[k] = lds[swz(tid + 256 * k)];
-    {
-        const u32 M0 = (N >> 12) + g;
-        inv_stage16<3>(v, itw, M0, q, q4);
-        inv_stage16<2>(v, itw, M0, q, q4);
-        inv_stage16<1>(v, itw, M0, q, q4);
-        inv_stage16<0>(v, itw, M0, q, q4);
-    }
+    for (int k = 0; k < 16; k++) v[k] = lds[L1 + 272 * k];
+    inv_round16(v, itw, (N >> 12) + g, M);
     if (logn == 12) {
 #pragma unroll
         for (int k = 0; k < 16; k++) v[k] = canon4(v[k], q);
@@ -275,74 +295,166 @@ __global__ __launch_bounds__(256) void k_block(PlanArgs P, const u64* src, u64* 
 }
 
 // ---------------------------------------------------------------------------
-// k_cols: the first KA = logN - 12 forward stages (or the last KA inverse
-// stages) on columns {c + 4096 k}, k < 2^KA, entirely in registers.
+// k_tcols: the first 8 forward stages (or the last 8 inverse stages) of an
+// N = 2^16 transform.  Element j = row * 256 + col; for a fixed col the 256
+// rows form one sub-transform.  A workgroup owns a tile of 16 columns x 256
+// rows (tile element p = row * 16 + col_in_tile) and runs the same two
+// radix-16 register rounds and padded LDS exchange as k_block's rounds 1-2:
+// twiddle indices depend on the row only (j / (2t) = row / (256/m)).  Global
+// accesses are 128-byte row segments.  With 8 column stages the pass has as
+// much multiply work as HBM time, instead of k_cols' 4 stages that leave the
+// VALU idle behind HBM.
 // ---------------------------------------------------------------------------
-template <int KA, bool INV>
-__global__ __launch_bounds__(256) void k_cols(PlanArgs P, const u64* src, u64* dst, u32 batch,
-                                              u32 nwg) {
-    constexpr int E = 1 << KA;
-    constexpr u32 N = 1u << (KA + 12);
+template <bool INV, bool SPQ>
+__global__ __launch_bounds__(256, OFHE_KB_WAVES) void k_tcols(PlanArgs P, const u64* src, u64* dst, u32 batch,
+                                                              u32 nwg) {
+    constexpr u32 N = 1u << 16, S = 256;
+    __shared__ u64 lds[LDS_WORDS];
+    const u32 tid = threadIdx.x;
     const u32 wid = xcd_remap(blockIdx.x, nwg);
-    const u32 cb = wid & 15;
-    const u32 pb = wid >> 4;
+    const u32 cb = wid % (S / 16);
+    const u32 pb = wid / (S / 16);
     const u32 t = pb / batch, b = pb % batch;
-    const u64 off = ((u64)b * P.towers + t) * N + cb * 256 + threadIdx.x;
+    const u64 off = ((u64)b * P.towers + t) * N + cb * 16;
     const u64* x = src + off;
     u64* y = dst + off;
-    const u64 q = P.tc[t].q, q3 = 3 * q, q4 = 4 * q;
-    u64 v[E];
-#pragma unroll
-    for (int k = 0; k < E; k++) v[k] = x[(u64)k * 4096];
+    const TowerConst tc = P.tc[t];
+    const u64 q = tc.q;
+    const Mod<SPQ> M = load_mod<SPQ>(tc);
+    const u32 h = tid >> 4, r = tid & 15;
+    const u32 L1 = tid + h, L2 = h * 272 + r;
+    u64 v[16];
     if (!INV) {
         const u64* tw = P.tw + (u64)t * N * 2;
+        // round 1: rows h + 16k (p = tid + 256k), stages m = 1..8
 #pragma unroll
-        for (int s = 0; s < KA; s++) {
-            const int half = E >> (s + 1);
+        for (int k = 0; k < 16; k++) v[k] = x[(u64)(h + 16 * k) * S + r];
+        fwd_round16(v, tw, 1, M);
 #pragma unroll
-            for (int j = 0; j < (1 << s); j++) {
-                Tw w = ldtw(tw, (1u << s) + j);
+        for (int k = 0; k < 16; k++) lds[L1 + 272 * k] = v[k];
+        __syncthreads();
+        // round 2: rows 16h + k (p = 256h + r + 16k), stages m = 16..128
 #pragma unroll
-                for (int k = j * 2 * half; k < j * 2 * half + half; k++)
-                    ct_bfly(v[k], v[k + half], w, q, q3, q4);
-            }
-        }
+        for (int k = 0; k < 16; k++) v[k] = lds[L2 + 17 * k];
+        fwd_round16(v, tw, 16 + h, M);
+#pragma unroll
+        for (int k = 0; k < 16; k++) y[(u64)(16 * h + k) * S + r] = v[k];
     } else {
         const u64* itw = P.itw + (u64)t * N * 2;
 #pragma unroll
-        for (int s = KA - 1; s >= 0; s--) {
-            const int half = E >> (s + 1);
+        for (int k = 0; k < 16; k++) v[k] = x[(u64)(16 * h + k) * S + r];
+        inv_round16(v, itw, 16 + h, M);
 #pragma unroll
-            for (int j = 0; j < (1 << s); j++) {
-                Tw w = ldtw(itw, (1u << s) + j);
+        for (int k = 0; k < 16; k++) lds[L2 + 17 * k] = v[k];
+        __syncthreads();
 #pragma unroll
-                for (int k = j * 2 * half; k < j * 2 * half + half; k++) gs_bfly(v[k], v[k + half], w, q, q4);
-            }
+        for (int k = 0; k < 16; k++) v[k] = lds[L1 + 272 * k];
+        inv_round16(v, itw, 1, M);
+#pragma unroll
+        for (int k = 0; k < 16; k++) y[(u64)(h + 16 * k) * S + r] = canon4(v[k], q);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// k_cols: the first KA = logN - 12 forward stages (or the last KA inverse
+// stages) on columns {c + 4096 k}, k < 2^KA, entirely in registers.  CPT
+// adjacent columns per thread make every global access 8*CPT bytes wide.
+// ---------------------------------------------------------------------------
+template <int E, int CPT, class M_>
+__device__ __forceinline__ void cols_fwd(u64 (&v)[CPT][E], const u64* tw, const M_& M) {
+    constexpr int KA = __builtin_ctz(E);
+#pragma unroll
+    for (int s = 0; s < KA; s++) {
+        const int half = E >> (s + 1);
+#pragma unroll
+        for (int j = 0; j < (1 << s); j++) {
+            Tw w = ldtw(tw, (1u << s) + j);
+#pragma unroll
+            for (int k = j * 2 * half; k < j * 2 * half + half; k++)
+#pragma unroll
+                for (int c = 0; c < CPT; c++) ct_bfly(v[c][k], v[c][k + half], w, M);
         }
+    }
+}
+template <int E, int CPT, class M_>
+__device__ __forceinline__ void cols_inv(u64 (&v)[CPT][E], const u64* itw, const M_& M) {
+    constexpr int KA = __builtin_ctz(E);
 #pragma unroll
-        for (int k = 0; k < E; k++) v[k] = canon4(v[k], q);
+    for (int s = KA - 1; s >= 0; s--) {
+        const int half = E >> (s + 1);
+#pragma unroll
+        for (int j = 0; j < (1 << s); j++) {
+            Tw w = ldtw(itw, (1u << s) + j);
+#pragma unroll
+            for (int k = j * 2 * half; k < j * 2 * half + half; k++)
+#pragma unroll
+                for (int c = 0; c < CPT; c++) gs_bfly(v[c][k], v[c][k + half], w, M);
+        }
+    }
+}
+
+template <int KA, bool INV, int CPT, bool SPQ>
+__global__ __launch_bounds__(256) void k_cols(PlanArgs P, const u64* src, u64* dst, u32 batch, u32 nwg) {
+    constexpr int E = 1 << KA;
+    constexpr u32 N = 1u << (KA + 12);
+    constexpr u32 CB = 16 / CPT;  // column blocks per polynomial
+    const u32 wid = xcd_remap(blockIdx.x, nwg);
+    const u32 cb = wid % CB;
+    const u32 pb = wid / CB;
+    const u32 t = pb / batch, b = pb % batch;
+    const u64 off = ((u64)b * P.towers + t) * N + cb * (256 * CPT) + threadIdx.x * CPT;
+    const u64* x = src + off;
+    u64* y = dst + off;
+    const TowerConst tc = P.tc[t];
+    const u64 q = tc.q;
+    const Mod<SPQ> M = load_mod<SPQ>(tc);
+    u64 v[CPT][E];
+#pragma unroll
+    for (int k = 0; k < E; k++) {
+        if (CPT == 2) {
+            const ulonglong2 p = *reinterpret_cast<const ulonglong2*>(x + (u64)k * 4096);
+            v[0][k] = p.x;
+            v[CPT - 1][k] = p.y;
+        } else {
+            v[0][k] = x[(u64)k * 4096];
+        }
+    }
+    if (!INV) {
+        cols_fwd<E, CPT>(v, P.tw + (u64)t * N * 2, M);
+    } else {
+        cols_inv<E, CPT>(v, P.itw + (u64)t * N * 2, M);
+#pragma unroll
+        for (int k = 0; k < E; k++)
+#pragma unroll
+            for (int c = 0; c < CPT; c++) v[c][k] = canon4(v[c][k], q);
     }
 #pragma unroll
-    for (int k = 0; k < E; k++) y[(u64)k * 4096] = v[k];
+    for (int k = 0; k < E; k++) {
+        if (CPT == 2)
+            *reinterpret_cast<ulonglong2*>(y + (u64)k * 4096) = make_ulonglong2(v[0][k], v[CPT - 1][k]);
+        else
+            y[(u64)k * 4096] = v[0][k];
+    }
 }
 
 // ---------------------------------------------------------------------------
 // k_small: N <= 2^11, one workgroup per polynomial, whole tower in LDS.
 // ---------------------------------------------------------------------------
-template <int MODE>
-__global__ __launch_bounds__(256) void k_small(PlanArgs P, const u64* src, u64* dst,
-                                               const u64* __restrict__ bdat, u32 batch) {
+template <int MODE, bool SPQ>
+__global__ __launch_bounds__(256) void k_small(PlanArgs P, const u64* src, u64* dst, const u64* __restrict__ bdat,
+                                               u32 batch) {
     __shared__ u64 lds[2048];
     const u32 logn = P.log_n, N = 1u << logn, half = N >> 1;
     const u32 pb = blockIdx.x;
-    const u32 b = pb / P.towers, t = pb % P.towers;
+    const u32 t = pb % P.towers;
     const u64 off = (u64)pb * N;
     const TowerConst tc = P.tc[t];
-    const u64 q = tc.q, q3 = 3 * q, q4 = 4 * q;
+    const u64 q = tc.q;
+    const Mod<SPQ> M = load_mod<SPQ>(tc);
     const u64* tw = P.tw + (u64)t * N * 2;
     const u64* itw = P.itw + (u64)t * N * 2;
     const u64* itwn = P.itwn + (u64)t * N;
-    (void)b;
+    (void)batch;
     for (u32 i = threadIdx.x; i < N; i += blockDim.x) lds[i] = src[off + i];
     __syncthreads();
     if (MODE == MODE_FWD || MODE == MODE_FUSED) {
@@ -351,7 +463,7 @@ __global__ __launch_bounds__(256) void k_small(PlanArgs P, const u64* src, u64* 
             for (u32 k = threadIdx.x; k < half; k += blockDim.x) {
                 const u32 i = k >> lt, j = (i << (lt + 1)) + (k & (tt - 1));
                 u64 x = lds[j], y = lds[j + tt];
-                ct_bfly(x, y, ldtw(tw, m + i), q, q3, q4);
+                ct_bfly(x, y, ldtw(tw, m + i), M);
                 lds[j] = x;
                 lds[j + tt] = y;
             }
@@ -374,9 +486,9 @@ __global__ __launch_bounds__(256) void k_small(PlanArgs P, const u64* src, u64* 
             const u32 i = k >> lt, j = (i << (lt + 1)) + (k & (tt - 1));
             u64 x = lds[j], y = lds[j + tt];
             if (m == half)
-                gs_bfly_ninv(x, y, ldtw(itwn, i), tc.ninv, tc.ninv_pre, q, q4);
+                gs_bfly_ninv(x, y, ldtw(itwn, i), tc.ninv, tc.ninv_pre, M);
             else
-                gs_bfly(x, y, ldtw(itw, m + i), q, q4);
+                gs_bfly(x, y, ldtw(itw, m + i), M);
             lds[j] = x;
             lds[j + tt] = y;
         }

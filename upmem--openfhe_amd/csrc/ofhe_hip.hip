@@ -14,6 +14,7 @@
 
 #include <atomic>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <new>
@@ -88,6 +89,13 @@ struct ofhe_plan_s {
     std::vector<u64> q, tab, tab_pre, itab, itab_pre, ninv;
     u64* d_scal = nullptr;  // scratch for per-tower scalars (modmul_scalar)
     std::mutex scal_mu;
+    // pipeline tuning (ofhe_hip_plan_tune): batch entries per chunk (0 = all)
+    // and internal streams the chunks alternate over (1 = caller's stream).
+    u32 chunk_batch = 0, nstreams = 1;
+    bool spq = false;     // every modulus is 2^L - d with d < 2^32 (special-prime kernels)
+    bool split8 = false;  // log_n == 16: 8 column stages + 8 block stages (k_tcols + k_block<.,.,2>)
+    hipStream_t st[2] = {nullptr, nullptr};
+    hipEvent_t ev_fork = nullptr, ev_join[2] = {nullptr, nullptr};
 };
 
 struct ofhe_bconv_s {
@@ -239,6 +247,10 @@ int ofhe_hip_plan_create(ofhe_ctx_t ctx, uint32_t log_n, uint32_t towers, const 
         const unsigned mb = msb64(qt);
         c.mu = (u64)((((u128)1) << (2 * mb + 3)) / qt);  // ComputeMu, ubintnat.h:651-656
         c.nshift = mb - 2;
+        // special prime q = 2^mb - d, d < 2^32: hi32(q) == 2^(mb-32) - 1
+        c.spq_sh = (mb >= 33 && (qt >> 32) == ((1ull << (mb - 32)) - 1)) ? mb - 32 : 0;
+        c.nq = 0 - qt;
+        c.nq4 = 0 - 4 * qt;
         tc[t] = c;
     };
     {
@@ -253,6 +265,10 @@ int ofhe_hip_plan_create(ofhe_ctx_t ctx, uint32_t log_n, uint32_t towers, const 
             });
         for (auto& x : th) x.join();
     }
+    p->spq = true;
+    for (u32 t = 0; t < towers; t++) p->spq = p->spq && tc[t].spq_sh != 0;
+    if (getenv("OFHE_NO_SPQ")) p->spq = false;  // A/B switch for tests and timing
+    p->split8 = log_n == 16 && !getenv("OFHE_SPLIT4");
     hipError_t e = hipSetDevice(ctx->device);
     if (e == hipSuccess) e = hipMalloc(&p->d_tc, sizeof(TowerConst) * towers);
     if (e == hipSuccess) e = hipMalloc(&p->d_tw, sizeof(u64) * 2 * TN);
@@ -271,9 +287,31 @@ int ofhe_hip_plan_create(ofhe_ctx_t ctx, uint32_t log_n, uint32_t towers, const 
     return OFHE_OK;
 }
 
+int ofhe_hip_plan_tune(ofhe_plan_t p, uint32_t chunk_batch, uint32_t streams) {
+    if (!p || !p->ctx) return fail(OFHE_ERR_STATE, "plan is NULL or destroyed");
+    if (streams < 1 || streams > 2) return fail(OFHE_ERR_ARG, "streams must be 1 or 2");
+    HIPCHK(hipSetDevice(p->ctx->device));
+    if (streams == 2 && !p->st[0]) {
+        for (int i = 0; i < 2; i++) {
+            HIPCHK(hipStreamCreateWithFlags(&p->st[i], hipStreamNonBlocking));
+            HIPCHK(hipEventCreateWithFlags(&p->ev_join[i], hipEventDisableTiming));
+        }
+        HIPCHK(hipEventCreateWithFlags(&p->ev_fork, hipEventDisableTiming));
+    }
+    p->chunk_batch = chunk_batch;
+    p->nstreams = streams;
+    return OFHE_OK;
+}
+
 int ofhe_hip_plan_destroy(ofhe_plan_t p) {
     if (!p) return fail(OFHE_ERR_ARG, "plan is NULL");
     if (p->ctx) (void)hipSetDevice(p->ctx->device);
+    for (int i = 0; i < 2; i++) {
+        if (p->st[i]) (void)hipStreamSynchronize(p->st[i]);
+        if (p->st[i]) (void)hipStreamDestroy(p->st[i]);
+        if (p->ev_join[i]) (void)hipEventDestroy(p->ev_join[i]);
+    }
+    if (p->ev_fork) (void)hipEventDestroy(p->ev_fork);
     (void)hipFree(p->d_tc);
     (void)hipFree(p->d_tw);
     (void)hipFree(p->d_itw);
@@ -318,38 +356,88 @@ static int check_common(ofhe_plan_t p, uint32_t batch) {
     return OFHE_OK;
 }
 
-template <int KA, bool INV>
+#ifndef OFHE_COLS_CPT
+#define OFHE_COLS_CPT 2
+#endif
+// Every launcher picks the special-prime instantiation when the plan allows it.
+template <int KA, bool INV, bool SPQ>
 static void launch_cols_t(const PlanArgs& a, const u64* src, u64* dst, u32 batch, hipStream_t s) {
-    const u32 nwg = batch * a.towers * 16;
-    hipLaunchKernelGGL((k_cols<KA, INV>), dim3(nwg), dim3(256), 0, s, a, src, dst, batch, nwg);
+    // two columns per thread (16-byte accesses) while registers allow
+    constexpr int CPT = KA <= 4 ? OFHE_COLS_CPT : 1;
+    const u32 nwg = batch * a.towers * (16 / CPT);
+    hipLaunchKernelGGL((k_cols<KA, INV, CPT, SPQ>), dim3(nwg), dim3(256), 0, s, a, src, dst, batch, nwg);
 }
 
-static void launch_cols(const PlanArgs& a, bool inv, const u64* src, u64* dst, u32 batch, hipStream_t s) {
+template <bool SPQ>
+static void launch_cols_s(const PlanArgs& a, bool inv, const u64* src, u64* dst, u32 batch, hipStream_t s) {
     switch (a.log_n - 12) {
-#define CASE(K)                                               \
-    case K:                                                   \
-        if (inv)                                              \
-            launch_cols_t<K, true>(a, src, dst, batch, s);    \
-        else                                                  \
-            launch_cols_t<K, false>(a, src, dst, batch, s);   \
+#define CASE(K)                                                 \
+    case K:                                                     \
+        if (inv)                                                \
+            launch_cols_t<K, true, SPQ>(a, src, dst, batch, s); \
+        else                                                    \
+            launch_cols_t<K, false, SPQ>(a, src, dst, batch, s);\
         break;
         CASE(1) CASE(2) CASE(3) CASE(4) CASE(5)
 #undef CASE
         default: break;
     }
 }
+static void launch_cols(const PlanArgs& a, bool spq, bool inv, const u64* src, u64* dst, u32 batch, hipStream_t s) {
+    if (spq)
+        launch_cols_s<true>(a, inv, src, dst, batch, s);
+    else
+        launch_cols_s<false>(a, inv, src, dst, batch, s);
+}
 
+// column pass for log_n > 12: k_tcols (8 stages) under split8, else k_cols
+static void launch_colpass(const PlanArgs& a, bool spq, bool split8, bool inv, const u64* src, u64* dst, u32 batch,
+                           hipStream_t s);
+
+// Pass split for log_n > 12: with split8 (log_n == 16) the column pass does 8
+// stages (k_tcols) and the block pass the last 8 (k_block NR=2); otherwise the
+// column pass does log_n - 12 stages in registers (k_cols) and the block pass 12.
 template <int MODE>
-static void launch_block(const PlanArgs& a, const u64* src, u64* dst, const u64* b, u32 batch, hipStream_t s) {
+static void launch_block(const PlanArgs& a, bool spq, const u64* src, u64* dst, const u64* b, u32 batch,
+                         hipStream_t s, bool split8 = false) {
     const u32 nwg = batch * a.towers * (1u << (a.log_n - 12));
-    hipLaunchKernelGGL((k_block<MODE>), dim3(nwg), dim3(256), 0, s, a, src, dst, b, batch, nwg);
+#define LB(SP, NR) hipLaunchKernelGGL((k_block<MODE, SP, NR>), dim3(nwg), dim3(256), 0, s, a, src, dst, b, batch, nwg)
+    if (split8) {
+        if (spq) LB(true, 2); else LB(false, 2);
+    } else {
+        if (spq) LB(true, 3); else LB(false, 3);
+    }
+#undef LB
+}
+
+static void launch_tcols(const PlanArgs& a, bool spq, bool inv, const u64* src, u64* dst, u32 batch, hipStream_t s) {
+    const u32 nwg = batch * a.towers * 16;
+#define LT(I, SP) hipLaunchKernelGGL((k_tcols<I, SP>), dim3(nwg), dim3(256), 0, s, a, src, dst, batch, nwg)
+    if (inv) {
+        if (spq) LT(true, true); else LT(true, false);
+    } else {
+        if (spq) LT(false, true); else LT(false, false);
+    }
+#undef LT
 }
 
 template <int MODE>
-static void launch_small(const PlanArgs& a, const u64* src, u64* dst, const u64* b, u32 batch, hipStream_t s) {
+static void launch_small(const PlanArgs& a, bool spq, const u64* src, u64* dst, const u64* b, u32 batch,
+                         hipStream_t s) {
     const u32 N = 1u << a.log_n;
     const u32 thr = N / 2 >= 256 ? 256 : (N / 2 < 64 ? 64 : N / 2);
-    hipLaunchKernelGGL((k_small<MODE>), dim3(batch * a.towers), dim3(thr), 0, s, a, src, dst, b, batch);
+    if (spq)
+        hipLaunchKernelGGL((k_small<MODE, true>), dim3(batch * a.towers), dim3(thr), 0, s, a, src, dst, b, batch);
+    else
+        hipLaunchKernelGGL((k_small<MODE, false>), dim3(batch * a.towers), dim3(thr), 0, s, a, src, dst, b, batch);
+}
+
+static void launch_colpass(const PlanArgs& a, bool spq, bool split8, bool inv, const u64* src, u64* dst, u32 batch,
+                           hipStream_t s) {
+    if (split8)
+        launch_tcols(a, spq, inv, src, dst, batch, s);
+    else
+        launch_cols(a, spq, inv, src, dst, batch, s);
 }
 
 static int post_launch() {
@@ -366,10 +454,10 @@ int ofhe_hip_ntt_fwd(ofhe_plan_t p, uint64_t* data, uint32_t batch, void* stream
     const PlanArgs a = args_of(p);
     hipStream_t s = pick(p->ctx, stream);
     if (p->log_n < 12) {
-        launch_small<MODE_FWD>(a, data, data, nullptr, batch, s);
+        launch_small<MODE_FWD>(a, p->spq, data, data, nullptr, batch, s);
     } else {
-        if (p->log_n > 12) launch_cols(a, false, data, data, batch, s);
-        launch_block<MODE_FWD>(a, data, data, nullptr, batch, s);
+        if (p->log_n > 12) launch_colpass(a, p->spq, p->split8, false, data, data, batch, s);
+        launch_block<MODE_FWD>(a, p->spq, data, data, nullptr, batch, s, p->split8);
     }
     return post_launch();
 }
@@ -382,10 +470,10 @@ int ofhe_hip_ntt_inv(ofhe_plan_t p, uint64_t* data, uint32_t batch, void* stream
     const PlanArgs a = args_of(p);
     hipStream_t s = pick(p->ctx, stream);
     if (p->log_n < 12) {
-        launch_small<MODE_INV>(a, data, data, nullptr, batch, s);
+        launch_small<MODE_INV>(a, p->spq, data, data, nullptr, batch, s);
     } else {
-        launch_block<MODE_INV>(a, data, data, nullptr, batch, s);
-        if (p->log_n > 12) launch_cols(a, true, data, data, batch, s);
+        launch_block<MODE_INV>(a, p->spq, data, data, nullptr, batch, s, p->split8);
+        if (p->log_n > 12) launch_colpass(a, p->spq, p->split8, true, data, data, batch, s);
     }
     return post_launch();
 }
@@ -400,13 +488,36 @@ int ofhe_hip_ntt_mul_intt(ofhe_plan_t p, const uint64_t* a_, const uint64_t* b, 
     const PlanArgs a = args_of(p);
     hipStream_t s = pick(p->ctx, stream);
     if (p->log_n < 12) {
-        launch_small<MODE_FUSED>(a, a_, c, b, batch, s);
+        launch_small<MODE_FUSED>(a, p->spq, a_, c, b, batch, s);
     } else if (p->log_n == 12) {
-        launch_block<MODE_FUSED>(a, a_, c, b, batch, s);
+        launch_block<MODE_FUSED>(a, p->spq, a_, c, b, batch, s, p->split8);
     } else {
-        launch_cols(a, false, a_, c, batch, s);
-        launch_block<MODE_FUSED>(a, c, c, b, batch, s);
-        launch_cols(a, true, c, c, batch, s);
+        // Chunk the batch so a chunk's intermediates stay in the Infinity
+        // Cache between the three passes; optionally alternate two streams so
+        // one chunk's HBM-bound column passes overlap another's VALU-bound
+        // block pass.
+        const u32 cb = (p->chunk_batch && p->chunk_batch < batch) ? p->chunk_batch : batch;
+        const u64 words = (u64)p->towers << p->log_n;
+        const bool multi = p->nstreams == 2 && cb < batch;
+        if (multi) {
+            HIPCHK(hipEventRecord(p->ev_fork, s));
+            for (int i = 0; i < 2; i++) HIPCHK(hipStreamWaitEvent(p->st[i], p->ev_fork, 0));
+        }
+        u32 idx = 0;
+        for (u32 b0 = 0; b0 < batch; b0 += cb, idx++) {
+            const u32 n = batch - b0 < cb ? batch - b0 : cb;
+            hipStream_t sx = multi ? p->st[idx & 1] : s;
+            const u64 off = (u64)b0 * words;
+            launch_colpass(a, p->spq, p->split8, false, a_ + off, c + off, n, sx);
+            launch_block<MODE_FUSED>(a, p->spq, c + off, c + off, b + off, n, sx, p->split8);
+            launch_colpass(a, p->spq, p->split8, true, c + off, c + off, n, sx);
+        }
+        if (multi) {
+            for (int i = 0; i < 2; i++) {
+                HIPCHK(hipEventRecord(p->ev_join[i], p->st[i]));
+                HIPCHK(hipStreamWaitEvent(s, p->ev_join[i], 0));
+            }
+        }
     }
     return post_launch();
 }
@@ -421,15 +532,15 @@ int ofhe_hip_ntt_mul_intt_stage(ofhe_plan_t p, int stage, const uint64_t* a_, co
     const PlanArgs a = args_of(p);
     hipStream_t s = pick(p->ctx, stream);
     if (p->log_n < 12) {
-        if (stage == 1) launch_small<MODE_FUSED>(a, a_, c, b, batch, s);
+        if (stage == 1) launch_small<MODE_FUSED>(a, p->spq, a_, c, b, batch, s);
     } else if (p->log_n == 12) {
-        if (stage == 1) launch_block<MODE_FUSED>(a, a_, c, b, batch, s);
+        if (stage == 1) launch_block<MODE_FUSED>(a, p->spq, a_, c, b, batch, s, p->split8);
     } else if (stage == 0) {
-        launch_cols(a, false, a_, c, batch, s);
+        launch_colpass(a, p->spq, p->split8, false, a_, c, batch, s);
     } else if (stage == 1) {
-        launch_block<MODE_FUSED>(a, c, c, b, batch, s);
+        launch_block<MODE_FUSED>(a, p->spq, c, c, b, batch, s, p->split8);
     } else {
-        launch_cols(a, true, c, c, batch, s);
+        launch_colpass(a, p->spq, p->split8, true, c, c, batch, s);
     }
     return post_launch();
 }

@@ -52,6 +52,7 @@ _SIGS = {
     "ofhe_hip_plan_create": (ctypes.c_int, [_vp, ctypes.c_uint32, ctypes.c_uint32, _u64p, _u64p,
                                             ctypes.POINTER(_vp)]),
     "ofhe_hip_plan_destroy": (ctypes.c_int, [_vp]),
+    "ofhe_hip_plan_tune": (ctypes.c_int, [_vp, ctypes.c_uint32, ctypes.c_uint32]),
     "ofhe_hip_plan_tables": (ctypes.c_int, [_vp, _u64p, _u64p, _u64p, _u64p, _u64p]),
     "ofhe_hip_ntt_fwd": (ctypes.c_int, [_vp, _vp, ctypes.c_uint32, _vp]),
     "ofhe_hip_ntt_inv": (ctypes.c_int, [_vp, _vp, ctypes.c_uint32, _vp]),
@@ -190,6 +191,10 @@ class NTTPlan:
             self.close()
         except Exception:
             pass
+
+    def tune(self, chunk_batch: int = 0, streams: int = 1) -> None:
+        """Chunking / stream knob of ntt_mul_intt (speed only; results are identical)."""
+        _check(lib().ofhe_hip_plan_tune(self.handle, int(chunk_batch), int(streams)))
 
     def tables(self):
         """Host copies of (Table, TableP, TableI, TableIP, ninv) as flat lists."""
