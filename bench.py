@@ -25,7 +25,7 @@ sys.path.insert(0, os.path.join(ROOT, "upmem--openfhe_amd"))
 METRIC = "64-bit coeffs/sec for NTT+Hadamard+INTT, N=2^16, 16 towers; % HBM roofline"
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8 TB/s spec
 ALG_BYTES_PER_COEFF = 24       # read a, read b, write c
-STAGE_NAMES = {0: "k_cols<fwd>", 1: "k_block<fused>", 2: "k_cols<inv>"}
+STAGE_NAMES = {0: "colpass<fwd>", 1: "k_block<fused>", 2: "colpass<inv>"}  # colpass = k_tcols (N=2^16) or k_cols
 
 
 def moduli_chain(log_n, towers, bits=60):
@@ -107,6 +107,11 @@ def main():
     torch.cuda.set_device(dev)
 
     import ofhe_hip as H
+    import shard
+
+    # weak scaling: every rank owns a batch shard of the same size
+    _, B_rank = shard.shard_batch(args.batch * world, rank, world)
+    assert B_rank == args.batch
 
     ctx = H.Context(local)
     log_n, T, B = args.log_n, args.towers, args.batch
@@ -126,17 +131,17 @@ def main():
     stream = torch.cuda.current_stream(dev)
     sp = stream.cuda_stream
 
-    # RCCL broadcast of a synthetic evaluation key (setup, outside the timed loop)
+    # RCCL broadcast of a synthetic hybrid key-switching key (configs[3]; setup,
+    # outside the timed loop -- the only collective the path has)
     bcast = None
     if world > 1:
-        dnum = 3
-        key = torch.empty((2 * dnum, T + (T + dnum - 1) // dnum, n), dtype=torch.int64, device=dev)
+        key = torch.empty(shard.evalkey_words(T, log_n, 3), dtype=torch.int64, device=dev)
         if rank == 0:
             key.random_(0, qs[-1], generator=g)
         dist.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        dist.broadcast(key, src=0)
+        shard.broadcast_evalkey(key, src=0)
         torch.cuda.synchronize()
         bcast = {"bytes": key.numel() * 8, "ms": (time.perf_counter() - t0) * 1e3, "backend": "nccl(RCCL)"}
         del key
@@ -158,9 +163,7 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     if world > 1:
-        e = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(e, op=dist.ReduceOp.MAX)
-        elapsed = float(e.item())
+        elapsed = shard.max_over_ranks(elapsed, device=dev)
     coeffs_per_step = B * T * n * world
     value = coeffs_per_step * args.steps / elapsed
     ms_per_step = elapsed / args.steps * 1e3

@@ -10,7 +10,8 @@ import os
 import sys
 
 d = sys.argv[1]
-NAMES = {"k_block<2>": "k_block<fused>", "k_cols<4, false": "k_cols<fwd>", "k_cols<4, true": "k_cols<inv>"}
+NAMES = {"k_block<2,": "k_block<fused>", "k_tcols<false": "colpass<fwd>", "k_tcols<true": "colpass<inv>",
+         "k_cols<4, false": "colpass<fwd>", "k_cols<4, true": "colpass<inv>"}
 out = {"source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes) on bench.py --steps 2",
        "correction": "hbm_bytes = 2*FETCH_SIZE*1024 + WRITE_SIZE*1024 (gfx950 FETCH_SIZE halving)",
        "kernels": {}}
