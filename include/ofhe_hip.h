@@ -10,8 +10,12 @@
  *   - NativeVectorT element-wise ModMul/ModAdd/ModSub
  *       (src/core/include/math/hal/intnat/mubintvecnat.h:426-432,501-513;
  *        src/core/lib/math/hal/intnat/mubintvecnat.cpp:245-367),
- *   - DCRTPolyImpl::ApproxSwitchCRTBasis
- *       (src/core/include/lattice/hal/default/dcrtpoly-impl.h:1034-1063).
+ *   - DCRTPolyImpl::ApproxSwitchCRTBasis / ApproxModUp / ApproxModDown
+ *       (src/core/include/lattice/hal/default/dcrtpoly-impl.h:1034-1175),
+ *   - the HYBRID key-switching core built on them
+ *       (src/pke/lib/keyswitch/keyswitch-hybrid.cpp:325-482),
+ *   - NativeVectorT::SwitchModulus and PolyImpl::AutomorphismTransform
+ *       (mubintvecnat.cpp:111-136, poly-impl.h:312-365).
  *
  * Conventions
  *   - Plain C, no exceptions cross the ABI. Every entry point returns an int
@@ -62,6 +66,13 @@ int ofhe_hip_finalize(ofhe_ctx_t ctx);
 /* PimManager::allocate / deallocate (PimManager.h:83-85) */
 int ofhe_hip_alloc(ofhe_ctx_t ctx, size_t bytes, void** dptr);
 int ofhe_hip_free(ofhe_ctx_t ctx, void* dptr);
+/* Stream-ordered variants (hipMallocAsync / hipFreeAsync): the block is
+ * released only after the work already queued on `stream` has finished, so a
+ * buffer can be dropped right after the asynchronous calls that use it. */
+int ofhe_hip_alloc_async(ofhe_ctx_t ctx, size_t bytes, void** dptr, void* stream);
+int ofhe_hip_free_async(ofhe_ctx_t ctx, void* dptr, void* stream);
+/* dst[0..bytes) = 0 on the stream (a zero DCRTPoly, dcrtpoly.h initializing ctor). */
+int ofhe_hip_zero(ofhe_ctx_t ctx, void* dst, size_t bytes, void* stream);
 /* PimManager::copy_to_pim (scatter, type 0) / copy_from_pim (PimManager.h:44-54) */
 int ofhe_hip_copy_to_device(ofhe_ctx_t ctx, void* dst, const void* src, size_t bytes, void* stream);
 int ofhe_hip_copy_to_host(ofhe_ctx_t ctx, void* dst, const void* src, size_t bytes, void* stream);
@@ -97,6 +108,18 @@ int ofhe_hip_ntt_fwd(ofhe_plan_t plan, uint64_t* data, uint32_t batch, void* str
 /* Inverse NTT in place, bit-reversed -> natural, n^-1 applied:
  * InverseTransformFromBitReverseInPlace (transformnat-impl.h:637-666 -> 492-552). */
 int ofhe_hip_ntt_inv(ofhe_plan_t plan, uint64_t* data, uint32_t batch, void* stream);
+
+/* The same transforms on plan towers [t0, t0 + count) of strided data, in or
+ * out of place: src / dst point at tower t0 of batch entry 0 and advance by
+ * src_stride / dst_stride words (>= count * N) per batch entry.  This is the
+ * per-tower SwitchFormat the DCRTPoly loops issue on sub-bases (e.g. the P
+ * towers of a Q|P polynomial in ApproxModUp, dcrtpoly-impl.h:1112-1116). */
+int ofhe_hip_ntt_fwd_range(ofhe_plan_t plan, uint32_t t0, uint32_t count, const uint64_t* src,
+                           uint64_t* dst, uint64_t src_stride, uint64_t dst_stride, uint32_t batch,
+                           void* stream);
+int ofhe_hip_ntt_inv_range(ofhe_plan_t plan, uint32_t t0, uint32_t count, const uint64_t* src,
+                           uint64_t* dst, uint64_t src_stride, uint64_t dst_stride, uint32_t batch,
+                           void* stream);
 
 /* c = a (op) b element-wise per tower: NativeVectorT::ModMul (Barrett,
  * mubintvecnat.cpp:353-367 / .h:501-513), ModAdd (.cpp:245-264 / .h:426-432),
@@ -141,6 +164,72 @@ int ofhe_hip_bconv_create(ofhe_ctx_t ctx, uint32_t log_n, uint32_t size_q, uint3
 int ofhe_hip_bconv_destroy(ofhe_bconv_t bconv);
 int ofhe_hip_approx_switch_crt_basis(ofhe_bconv_t bconv, const uint64_t* x, uint64_t* out,
                                      uint32_t batch, void* stream);
+
+/* DCRTPolyImpl::ApproxModUp (dcrtpoly-impl.h:1085-1131).  x: [batch][Q][N]
+ * under plan_q, in evaluation form when eval_form != 0 (else coefficient
+ * form); out: [batch][Q+P][N] in evaluation form, towers Q of plan_q then P
+ * of plan_p.  q_to_p converts plan_q's basis to plan_p's.  out must not
+ * overlap x. */
+int ofhe_hip_approx_mod_up(ofhe_plan_t plan_q, ofhe_plan_t plan_p, ofhe_bconv_t q_to_p, int eval_form,
+                           const uint64_t* x, uint64_t* out, uint32_t batch, void* stream);
+/* DCRTPolyImpl::ApproxModDown (dcrtpoly-impl.h:1134-1175).  x: [batch][Q+P][N]
+ * evaluation form; out: [batch][Q][N] evaluation form.  p_to_q converts
+ * plan_p's basis to plan_q's (PHatInvModp, PHatModq); p_inv_modq: host
+ * [Q] = P^-1 mod q_i.  t = 0 for CKKS / BFV; t > 0 (BGV) multiplies the P part
+ * by t^-1 mod p_j and the switched part by t (t_inv_modp derived here).
+ * Synchronises `stream` once to stage its small constant tables. */
+int ofhe_hip_approx_mod_down(ofhe_plan_t plan_q, ofhe_plan_t plan_p, ofhe_bconv_t p_to_q,
+                             const uint64_t* p_inv_modq, uint64_t t, const uint64_t* x, uint64_t* out,
+                             uint32_t batch, void* stream);
+
+/* ---- HYBRID key switching: KeySwitchHYBRID (pke/lib/keyswitch/
+ *      keyswitch-hybrid.cpp:325-482) with the CRT tables of
+ *      CryptoParametersRNS::PrecomputeCRTTables (pke/lib/schemerns/
+ *      rns-cryptoparameters.cpp:72-345) built internally from the moduli.
+ *      Q = q[0..size_q) (element params), P = p[0..size_p) (GetParamsP()),
+ *      num_part_q = dnum digits of alpha = ceil(size_q / num_part_q) towers.
+ *      Every call works at level size_ql (1 <= size_ql <= size_q): the
+ *      ciphertext has towers q[0..size_ql).  Evaluation keys are laid out
+ *      [num_part_q][size_q + size_p][N] (EvalKey b / a vectors over QP),
+ *      shared by the batch. ---- */
+typedef struct ofhe_ks_s* ofhe_ks_t;
+int ofhe_hip_ks_create(ofhe_ctx_t ctx, uint32_t log_n, uint32_t size_q, const uint64_t* q,
+                       const uint64_t* psi_q, uint32_t size_p, const uint64_t* p, const uint64_t* psi_p,
+                       uint32_t num_part_q, ofhe_ks_t* ks);
+int ofhe_hip_ks_destroy(ofhe_ks_t ks);
+/* alpha (towers per digit) and beta (digits at level size_ql, capped at
+ * num_part_q), keyswitch-hybrid.cpp:341-345. */
+int ofhe_hip_ks_digits(ofhe_ks_t ks, uint32_t size_ql, uint32_t* alpha, uint32_t* beta);
+/* EvalKeySwitchPrecomputeCore (keyswitch-hybrid.cpp:330-412): c [batch][size_ql][N]
+ * evaluation form -> digits [batch][beta][size_ql + size_p][N] evaluation form. */
+int ofhe_hip_ks_precompute(ofhe_ks_t ks, uint32_t size_ql, const uint64_t* c, uint64_t* digits,
+                           uint32_t batch, void* stream);
+/* EvalFastKeySwitchCoreExt (keyswitch-hybrid.cpp:438-482): ct0 = sum_j digits_j * b_j,
+ * ct1 = sum_j digits_j * a_j over Ql|P; ct0, ct1: [batch][size_ql + size_p][N]. */
+int ofhe_hip_ks_fast_core_ext(ofhe_ks_t ks, uint32_t size_ql, const uint64_t* digits,
+                              const uint64_t* key_b, const uint64_t* key_a, uint64_t* ct0, uint64_t* ct1,
+                              uint32_t batch, void* stream);
+/* ApproxModDown with the key-switching tables (keyswitch-hybrid.cpp:423-435):
+ * x [batch][size_ql + size_p][N] -> out [batch][size_ql][N], evaluation form. */
+int ofhe_hip_ks_mod_down(ofhe_ks_t ks, uint32_t size_ql, const uint64_t* x, uint64_t* out, uint64_t t,
+                         uint32_t batch, void* stream);
+/* KeySwitchCore = EvalFastKeySwitchCore(EvalKeySwitchPrecomputeCore(c))
+ * (keyswitch-hybrid.cpp:325-328, 414-436): out0, out1 [batch][size_ql][N]. */
+int ofhe_hip_ks_core(ofhe_ks_t ks, uint32_t size_ql, const uint64_t* c, const uint64_t* key_b,
+                     const uint64_t* key_a, uint64_t* out0, uint64_t* out1, uint64_t t, uint32_t batch,
+                     void* stream);
+
+/* ---- element maps ---- */
+/* NativeVectorT::SwitchModulus (mubintvecnat.cpp:111-136) on n words:
+ * values of modulus old_q re-centred to new_q, exactly as the reference. */
+int ofhe_hip_switch_modulus(ofhe_ctx_t ctx, const uint64_t* src, uint64_t* dst, uint64_t n,
+                            uint64_t old_q, uint64_t new_q, void* stream);
+/* PolyImpl::AutomorphismTransform(k) (poly-impl.h:312-365), X -> X^k for odd
+ * k, per (batch, tower) of plan; eval_form != 0 permutes bit-reversed
+ * evaluation slots, else signed permutation of coefficients (a negated zero
+ * stays q, as in the reference).  dst must not overlap src. */
+int ofhe_hip_automorphism(ofhe_plan_t plan, uint32_t k, int eval_form, const uint64_t* src, uint64_t* dst,
+                          uint32_t batch, void* stream);
 
 #ifdef __cplusplus
 }

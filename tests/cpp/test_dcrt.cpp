@@ -1,6 +1,7 @@
 // C++ parity tests through the host adapter (upmem--openfhe_amd/host/ofhe_dcrt.hpp)
 // and the C ABI, written like the reference's own gtest suites (gtest is an
 // empty submodule in the reference, so this is a minimal self-contained runner).
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 #include <functional>
@@ -95,6 +96,29 @@ static std::shared_ptr<DCRTParams> params(uint32_t m, const std::vector<uint64_t
     std::vector<uint64_t> r;
     for (auto x : q) r.push_back(root_of_unity(m, x));
     return std::make_shared<DCRTParams>(m, q, r);
+}
+// prod_{k != skip} v[k] mod m  (CRT tables as residues of products)
+static uint64_t prod_mod(const std::vector<uint64_t>& v, size_t skip, uint64_t m) {
+    uint64_t r = 1 % m;
+    for (size_t k = 0; k < v.size(); k++)
+        if (k != skip) r = mulmod(r, v[k] % m, m);
+    return r;
+}
+static std::unique_ptr<BaseConverter> converter(const DCRTParams& A, const DCRTParams& B) {
+    std::vector<uint64_t> hinv, hmod;
+    const auto& a = A.Moduli();
+    for (size_t i = 0; i < a.size(); i++) {
+        hinv.push_back(powmod(prod_mod(a, i, a[i]), a[i] - 2, a[i]));
+        for (auto bj : B.Moduli()) hmod.push_back(prod_mod(a, i, bj));
+    }
+    return std::unique_ptr<BaseConverter>(new BaseConverter(A, B, hinv, hmod));
+}
+// signed small coefficients -> residues per tower, [towers][n]
+static std::vector<uint64_t> signed_residues(const std::vector<int64_t>& c, const std::vector<uint64_t>& q) {
+    std::vector<uint64_t> out;
+    for (auto qt : q)
+        for (auto v : c) out.push_back(v >= 0 ? (uint64_t)v % qt : qt - (uint64_t)(-v) % qt);
+    return out;
 }
 
 static void TEST(const char* name, const std::function<void()>& f) {
@@ -223,6 +247,128 @@ int main() {
             ok = ok && r[i] == (uint64_t)((u128)a[i] * (sc[t] % q[t]) % q[t]);
         }
         EXPECT_EQ(ok, true, "scalar Times");
+    });
+    // ApproxModDown(P * ApproxModUp(x)) == x (dcrtpoly-impl.h:1085-1175), N = 2^12
+    TEST("DCRTPolyHip.mod_down_inverts_p_times_mod_up", [] {
+        const uint32_t m = 1u << 13;
+        std::vector<uint64_t> all;
+        uint64_t x = first_prime(60, m);
+        for (int t = 0; t < 6; t++) all.push_back(x = previous_prime(x, m));
+        std::vector<uint64_t> q(all.begin(), all.begin() + 4), p(all.begin() + 4, all.end());
+        auto PQ = params(m, q), PP = params(m, p), PQP = params(m, all);
+        auto up = converter(*PQ, *PP), down = converter(*PP, *PQ);
+        std::vector<uint64_t> pinv, pmod;
+        for (auto qi : q) pinv.push_back(powmod(prod_mod(p, p.size(), qi), qi - 2, qi));
+        for (auto mm : all) pmod.push_back(prod_mod(p, p.size(), mm));
+        std::mt19937_64 rng(5);
+        const uint32_t batch = 2, n = m / 2;
+        std::vector<uint64_t> v((size_t)batch * 4 * n);
+        for (size_t i = 0; i < v.size(); i++) v[i] = rng() % q[(i / n) % 4];
+        DCRTPolyHip X(PQ, Format::EVALUATION, batch);
+        X.SetValues(v, Format::EVALUATION);
+        DCRTPolyHip U = ApproxModUp(X, PP, PQP, *up);
+        EXPECT_EQ(U.GetFormat() == Format::EVALUATION, true, "ModUp output format");
+        DCRTPolyHip Y = ApproxModDown(U.Times(pmod), PQ, PP, *down, pinv);
+        EXPECT_EQ(Y, X, "ModDown(P * ModUp(x))");
+        DCRTPolyHip Yb = ApproxModDown(U.Times(pmod), PQ, PP, *down, pinv, 65537);  // temporary operand
+        EXPECT_EQ(Yb, X, "same with BGV t");
+        if (!(Yb == X)) {
+            auto a = Yb.GetValues(), b = X.GetValues();
+            size_t bad = 0, first = a.size();
+            for (size_t i = 0; i < a.size(); i++)
+                if (a[i] != b[i]) bad++, first = std::min(first, i);
+            std::printf("  %zu/%zu differ, first at %zu (batch %zu tower %zu): %llu vs %llu\n", bad, a.size(), first,
+                        first / (4 * n), (first / n) % 4, (unsigned long long)a[first], (unsigned long long)b[first]);
+        }
+        EXPECT_THROW(ApproxModDown(X, PQ, PP, *down, pinv), math_error, "ModDown on a Q-only polynomial");
+    });
+    // KeySwitchCore with keys as KeySwitchGenInternal builds them
+    // (keyswitch-hybrid.cpp:53-128): ct0 + ct1 s_new = c s_old + small.
+    TEST("KeySwitchHybrid.core_semantics", [] {
+        const uint32_t m = 1u << 11, n = m / 2, dnum = 2;
+        std::vector<uint64_t> all;
+        uint64_t x = first_prime(60, m);
+        for (int t = 0; t < 6; t++) all.push_back(x = previous_prime(x, m));
+        std::vector<uint64_t> q(all.begin(), all.begin() + 4), p(all.begin() + 4, all.end());
+        auto PQ = params(m, q), PP = params(m, p), PQP = params(m, all);
+        KeySwitchHybrid ks(*PQ, *PP, dnum);
+        std::mt19937_64 rng(9);
+        std::vector<int64_t> so(n), sn(n);
+        for (auto& v : so) v = (int64_t)(rng() % 3) - 1;
+        for (auto& v : sn) v = (int64_t)(rng() % 3) - 1;
+        DCRTPolyHip SnQP(PQP, Format::COEFFICIENT), SoQ(PQ, Format::COEFFICIENT);
+        SnQP.SetValues(signed_residues(sn, all), Format::COEFFICIENT);
+        SoQ.SetValues(signed_residues(so, q), Format::COEFFICIENT);
+        SnQP.SwitchFormat();
+        SoQ.SwitchFormat();
+        auto sn_e = SnQP.GetValues(), so_e = SoQ.GetValues();
+        std::vector<uint64_t> kb, ka;
+        for (uint32_t part = 0; part < dnum; part++) {
+            std::vector<int64_t> e(n);
+            for (auto& v : e) v = (int64_t)(rng() % 7) - 3;
+            DCRTPolyHip E(PQP, Format::COEFFICIENT);
+            E.SetValues(signed_residues(e, all), Format::COEFFICIENT);
+            E.SwitchFormat();
+            auto ev = E.GetValues();
+            for (size_t i = 0; i < all.size(); i++) {
+                const uint64_t mi = all[i], pm = prod_mod(p, p.size(), mi);
+                const bool in_digit = i >= part * 2 && i < part * 2 + 2;
+                for (uint32_t c = 0; c < n; c++) {
+                    const uint64_t a = rng() % mi, k = i * n + c;
+                    uint64_t b = (mi - mulmod(a, sn_e[k], mi)) % mi;
+                    if (in_digit) b = (b + mulmod(pm, so_e[k], mi)) % mi;
+                    b = (b + ev[k]) % mi;
+                    kb.push_back(b);
+                    ka.push_back(a);
+                }
+            }
+        }
+        DCRTPolyHip KB(PQP, Format::EVALUATION, dnum), KA(PQP, Format::EVALUATION, dnum);
+        KB.SetValues(kb, Format::EVALUATION);
+        KA.SetValues(ka, Format::EVALUATION);
+        DCRTPolyHip C(PQ, Format::EVALUATION);
+        std::vector<uint64_t> cv(4 * n);
+        for (size_t i = 0; i < cv.size(); i++) cv[i] = rng() % q[i / n];
+        C.SetValues(cv, Format::EVALUATION);
+        auto r = ks.KeySwitchCore(C, KB, KA);
+        std::vector<uint64_t> sq(sn_e.begin(), sn_e.begin() + 4 * n);
+        DCRTPolyHip SnQ(PQ, Format::EVALUATION);
+        SnQ.SetValues(sq, Format::EVALUATION);
+        DCRTPolyHip D = (r.first + r.second * SnQ) - C * SoQ;
+        D.SwitchFormat();
+        auto d = D.GetValues();
+        bool small = true, consistent = true;
+        for (uint32_t c = 0; c < n; c++) {
+            int64_t v0 = 0;
+            for (size_t t = 0; t < 4; t++) {
+                const uint64_t u = d[t * n + c];
+                const int64_t v = u > q[t] / 2 ? -(int64_t)(q[t] - u) : (int64_t)u;
+                small = small && (v < (1 << 20) && v > -(1 << 20));
+                if (t == 0) v0 = v;
+                consistent = consistent && v == v0;
+            }
+        }
+        EXPECT_EQ(small, true, "error is small");
+        EXPECT_EQ(consistent, true, "error is the same integer in every tower");
+        EXPECT_THROW(ks.KeySwitchCore(C, SnQP, KA), math_error, "wrong key shape");
+    });
+    // AutomorphismTransform: sigma_k then sigma_k^-1 is the identity, both forms
+    TEST("DCRTPolyHip.automorphism_inverse", [] {
+        const uint32_t m = 1u << 12, n = m / 2;
+        auto P = params(m, {first_prime(50, m), next_prime(first_prime(50, m), m)});
+        std::mt19937_64 rng(4);
+        std::vector<uint64_t> v(2 * n);
+        for (size_t i = 0; i < v.size(); i++) v[i] = 1 + rng() % (P->Moduli()[i / n] - 1);  // no zeros
+        const uint32_t k = 5;
+        uint32_t kinv = 1;
+        while ((uint64_t)k * kinv % m != 1) kinv += 2;
+        for (Format f : {Format::EVALUATION, Format::COEFFICIENT}) {
+            DCRTPolyHip X(P, f);
+            X.SetValues(v, f);
+            EXPECT_EQ(X.AutomorphismTransform(k).AutomorphismTransform(kinv), X, "sigma_kinv(sigma_k(x))");
+        }
+        DCRTPolyHip X(P, Format::EVALUATION);
+        EXPECT_THROW(X.AutomorphismTransform(4), math_error, "even index");
     });
     // error behaviour: OPENFHE_THROW analogues
     TEST("DCRTPolyHip.errors", [] {

@@ -1,0 +1,332 @@
+"""GPU parity for SURVEY.md §8(f) rows 1-3 through the C ABI: tower-range
+NTTs, ApproxModUp / ApproxModDown, HYBRID key switching (precompute, inner
+product, ModDown, KeySwitchCore), SwitchModulus and AutomorphismTransform.
+Bit-exact against oracle/keyswitch.py, whose restatement is pinned by
+tests/test_keyswitch_oracle.py (exact identities + a semantic key-switch test).
+"""
+import numpy as np
+import pytest
+
+import keyswitch as K
+import oracle as O
+from test_gpu_parity import dev, host, stream
+
+pytestmark = pytest.mark.gpu
+
+
+def _bases(log_n, sq, sp):
+    m, r = O.moduli_chain(log_n, sq + sp)
+    return m[:sq], r[:sq], m[sq:], r[sq:]
+
+
+def _generic_bases(log_n, sq, sp):
+    """moduli far from 2^60 (no special-prime form): exercises Mod<false>."""
+    m = 2 << log_n
+    qs, rs = [], []
+    x = O.next_prime((1 << 50) + 1 + 12345 * m, m)  # candidates = 1 mod 2N
+    while len(qs) < sq + sp:
+        qs.append(x)
+        rs.append(O.root_of_unity(m, x))
+        x = O.next_prime(x + 977 * m, m)
+    return qs[:sq], rs[:sq], qs[sq:], rs[sq:]
+
+
+def _uniform(rng, batch, moduli, n):
+    return np.stack([np.stack([rng.integers(0, m, size=n, dtype=np.uint64) for m in moduli])
+                     for _ in range(batch)])
+
+
+@pytest.mark.parametrize("log_n", [4, 11, 12, 13, 16])
+def test_range_transforms_strided(hip, log_n):
+    H, ctx = hip
+    import torch
+
+    n = 1 << log_n
+    q, r = O.moduli_chain(log_n, 5)
+    plan = H.NTTPlan(ctx, log_n, q, r)
+    rng = np.random.default_rng(log_n)
+    B = 2
+    x = _uniform(rng, B, q, n)
+    # towers [1, 4) of a 5-tower polynomial into a 7-tower-wide buffer at tower 2
+    src = dev(x)
+    dst = torch.zeros((B, 7, n), dtype=torch.int64, device="cuda")
+    plan.forward_range(1, 3, src[:, 1].data_ptr(), dst[:, 2].data_ptr(), 5 * n, 7 * n, B, stream())
+    got = host(dst)
+    ref = K.set_format(x[:, 1:4], q[1:4], r[1:4], True)
+    assert np.array_equal(got[:, 2:5], ref)
+    assert not got[:, :2].any() and not got[:, 5:].any()
+    back = torch.zeros((B, 3, n), dtype=torch.int64, device="cuda")
+    plan.inverse_range(1, 3, dst[:, 2].data_ptr(), back.data_ptr(), 7 * n, 3 * n, B, stream())
+    assert np.array_equal(host(back), x[:, 1:4])
+    # in place on a strided view
+    y = dev(x)
+    plan.forward_range(4, 1, y[:, 4].data_ptr(), y[:, 4].data_ptr(), 5 * n, 5 * n, B, stream())
+    g = host(y)
+    assert np.array_equal(g[:, 4:], K.set_format(x[:, 4:], q[4:], r[4:], True))
+    assert np.array_equal(g[:, :4], x[:, :4])
+
+
+def test_range_errors(hip):
+    H, ctx = hip
+    import torch
+
+    q, r = O.moduli_chain(6, 2)
+    plan = H.NTTPlan(ctx, 6, q, r)
+    x = torch.zeros((1, 2, 64), dtype=torch.int64, device="cuda")
+    with pytest.raises(H.MathError):
+        plan.forward_range(1, 2, x.data_ptr(), x.data_ptr(), 128, 128, 1, stream())
+    with pytest.raises(H.MathError):
+        plan.forward_range(0, 2, x.data_ptr(), x.data_ptr(), 64, 128, 1, stream())
+
+
+def _converter(H, ctx, log_n, src, dst):
+    qhinv, qhmodp = K.switch_tables(src, dst)
+    return H.BaseConverter(ctx, log_n, src, dst, qhinv, [v for row in qhmodp for v in row])
+
+
+@pytest.mark.parametrize("log_n,sq,sp,generic", [(5, 3, 2, False), (12, 4, 2, False), (13, 3, 3, True),
+                                                 (16, 4, 2, False)])
+@pytest.mark.parametrize("eval_form", [True, False])
+def test_approx_mod_up(hip, log_n, sq, sp, generic, eval_form):
+    H, ctx = hip
+    import torch
+
+    n = 1 << log_n
+    q, rq, p, rp = (_generic_bases if generic else _bases)(log_n, sq, sp)
+    pq, pp = H.NTTPlan(ctx, log_n, q, rq), H.NTTPlan(ctx, log_n, p, rp)
+    bc = _converter(H, ctx, log_n, q, p)
+    rng = np.random.default_rng(3 + log_n)
+    B = 2
+    x = _uniform(rng, B, q, n)
+    if eval_form:
+        x = K.set_format(x, q, rq, True)
+    out = torch.empty((B, sq + sp, n), dtype=torch.int64, device="cuda")
+    dx = dev(x)  # keep device inputs referenced until the stream has consumed them
+    H.approx_mod_up(pq, pp, bc, eval_form, dx.data_ptr(), out.data_ptr(), B, stream())
+    assert np.array_equal(host(out), K.approx_mod_up(x, q, rq, p, rp, eval_form))
+
+
+@pytest.mark.parametrize("log_n,sq,sp,generic", [(5, 3, 2, False), (12, 4, 2, True), (14, 5, 3, False)])
+@pytest.mark.parametrize("t", [0, 65537])
+def test_approx_mod_down(hip, log_n, sq, sp, generic, t):
+    H, ctx = hip
+    import torch
+
+    n = 1 << log_n
+    q, rq, p, rp = (_generic_bases if generic else _bases)(log_n, sq, sp)
+    pq, pp = H.NTTPlan(ctx, log_n, q, rq), H.NTTPlan(ctx, log_n, p, rp)
+    bc = _converter(H, ctx, log_n, p, q)
+    T = K.moddown_tables(q, p, t)
+    rng = np.random.default_rng(5 + log_n + t)
+    B = 3
+    x = _uniform(rng, B, q + p, n)
+    out = torch.empty((B, sq, n), dtype=torch.int64, device="cuda")
+    dx = dev(x)
+    H.approx_mod_down(pq, pp, bc, T["pinv_modq"], t, dx.data_ptr(), out.data_ptr(), B, stream())
+    assert np.array_equal(host(out), K.approx_mod_down(x, q, rq, p, rp, t))
+
+
+def _ks_case(H, ctx, log_n, sq, sp, dnum, generic=False):
+    n = 1 << log_n
+    q, rq, p, rp = (_generic_bases if generic else _bases)(log_n, sq, sp)
+    kp = K.KeySwitchParams(n, q, rq, p, rp, dnum)
+    ks = H.KeySwitch(ctx, log_n, q, rq, p, rp, dnum)
+    return n, q, rq, p, rp, kp, ks
+
+
+KS_CASES = [
+    (4, 4, 2, 2, False),    # tiny ring, two full digits
+    (6, 5, 3, 2, False),    # partial last digit (alpha = 3)
+    (12, 6, 2, 3, True),    # generic moduli
+    (13, 8, 3, 3, False),   # alpha = 3, digits 3+3+2
+    (16, 6, 2, 3, False),   # N = 2^16 (8|8 split transforms)
+]
+
+
+@pytest.mark.parametrize("log_n,sq,sp,dnum,generic", KS_CASES)
+def test_keyswitch_steps(hip, log_n, sq, sp, dnum, generic):
+    H, ctx = hip
+    import torch
+
+    n, q, rq, p, rp, kp, ks = _ks_case(H, ctx, log_n, sq, sp, dnum, generic)
+    rng = np.random.default_rng(100 + log_n)
+    B = 2
+    for l in sorted({sq, max(1, sq - 1), max(1, kp.alpha - 1)}, reverse=True):
+        alpha, beta = ks.digits(l)
+        assert (alpha, beta) == (kp.alpha, kp.beta(l))
+        c = K.set_format(_uniform(rng, B, q[:l], n), q[:l], rq[:l], True)
+        d = torch.empty((B, beta, l + sp, n), dtype=torch.int64, device="cuda")
+        dc = dev(c)
+        ks.precompute(l, dc.data_ptr(), d.data_ptr(), B, stream())
+        dref = K.ks_precompute(kp, c)
+        assert np.array_equal(host(d), dref), f"precompute level {l}"
+        kb = _uniform(rng, dnum, q + p, n)
+        ka = _uniform(rng, dnum, q + p, n)
+        c0 = torch.empty((B, l + sp, n), dtype=torch.int64, device="cuda")
+        c1 = torch.empty_like(c0)
+        dd, dkb, dka = dev(dref), dev(kb), dev(ka)
+        ks.fast_core_ext(l, dd.data_ptr(), dkb.data_ptr(), dka.data_ptr(), c0.data_ptr(), c1.data_ptr(), B,
+                         stream())
+        r0, r1 = K.ks_fast_core_ext(kp, dref, kb, ka)
+        assert np.array_equal(host(c0), r0) and np.array_equal(host(c1), r1), f"inner product level {l}"
+        for t in (0, 65537):
+            o = torch.empty((B, l, n), dtype=torch.int64, device="cuda")
+            dr = dev(r0)
+            ks.mod_down(l, dr.data_ptr(), o.data_ptr(), t, B, stream())
+            assert np.array_equal(host(o), K.ks_mod_down(kp, r0, t)), f"mod down level {l} t {t}"
+
+
+@pytest.mark.parametrize("log_n,sq,sp,dnum,generic", KS_CASES[:3])
+def test_keyswitch_core_semantics(hip, log_n, sq, sp, dnum, generic):
+    """KeySwitchCore on the GPU with real keys: equals the oracle bit for bit
+    and satisfies ct0 + ct1*s_new = c*s_old + small."""
+    H, ctx = hip
+    import torch
+
+    n, q, rq, p, rp, kp, ks = _ks_case(H, ctx, log_n, sq, sp, dnum, generic)
+    rng = np.random.default_rng(7)
+    s_old, s_new = K.ternary(n, rng), K.ternary(n, rng)
+    kb, ka = K.keyswitch_gen(kp, s_old, s_new, rng)
+    B = 2
+    c = K.set_format(_uniform(rng, B, q, n), q, rq, True)
+    o0 = torch.empty((B, sq, n), dtype=torch.int64, device="cuda")
+    o1 = torch.empty_like(o0)
+    dc, dkb, dka = dev(c), dev(kb), dev(ka)
+    ks.core(sq, dc.data_ptr(), dkb.data_ptr(), dka.data_ptr(), o0.data_ptr(), o1.data_ptr(), 0, B, stream())
+    g0, g1 = host(o0), host(o1)
+    r0, r1 = K.ks_core(kp, c, kb, ka)
+    assert np.array_equal(g0, r0) and np.array_equal(g1, r1)
+    sn = np.repeat(K.small_poly_eval(s_new, q, rq), B, 0)
+    so = np.repeat(K.small_poly_eval(s_old, q, rq), B, 0)
+    lhs = O.eltwise("add", g0, O.eltwise("mul", g1, sn, q), q)
+    d = K.set_format(O.eltwise("sub", lhs, O.eltwise("mul", c, so, q), q), q, rq, False)
+    for b in range(B):
+        assert max(abs(e) for e in K.crt_centered(d[b], q)) < 1 << 20
+
+
+def test_keyswitch_bootstrap_shape(hip):
+    """configs[4] shape: N = 2^17, 48 Q towers, dnum = 3 (alpha = 16), P = 16
+    towers (sizeP = ceil(16*60 / 60)), one ciphertext, full level."""
+    H, ctx = hip
+    import torch
+
+    log_n, sq, sp, dnum = 17, 48, 16, 3
+    n, q, rq, p, rp, kp, ks = _ks_case(H, ctx, log_n, sq, sp, dnum)
+    rng = np.random.default_rng(17)
+    c = K.set_format(_uniform(rng, 1, q, n), q, rq, True)
+    kb = _uniform(rng, dnum, q + p, n)
+    ka = _uniform(rng, dnum, q + p, n)
+    o0 = torch.empty((1, sq, n), dtype=torch.int64, device="cuda")
+    o1 = torch.empty_like(o0)
+    dc, dkb, dka = dev(c), dev(kb), dev(ka)
+    ks.core(sq, dc.data_ptr(), dkb.data_ptr(), dka.data_ptr(), o0.data_ptr(), o1.data_ptr(), 0, 1, stream())
+    r0, r1 = K.ks_core(kp, c, kb, ka)
+    assert np.array_equal(host(o0), r0) and np.array_equal(host(o1), r1)
+
+
+@pytest.mark.parametrize("t", [0, 65537])
+def test_mod_down_of_p_times_mod_up_full_size(hip, t):
+    """Size-independent identity at N = 2^16, 16 towers: ModDown(P * ModUp(x)) = x."""
+    H, ctx = hip
+    import torch
+
+    log_n, sq, sp = 16, 16, 4
+    n = 1 << log_n
+    q, rq, p, rp = _bases(log_n, sq, sp)
+    pq, pp = H.NTTPlan(ctx, log_n, q, rq), H.NTTPlan(ctx, log_n, p, rp)
+    pqp = H.NTTPlan(ctx, log_n, q + p, rq + rp)
+    up_bc, down_bc = _converter(H, ctx, log_n, q, p), _converter(H, ctx, log_n, p, q)
+    T = K.moddown_tables(q, p)
+    B = 4
+    x = torch.empty((B, sq, n), dtype=torch.int64, device="cuda")
+    for t in range(sq):
+        x[:, t].random_(0, q[t])
+    up = torch.empty((B, sq + sp, n), dtype=torch.int64, device="cuda")
+    H.approx_mod_up(pq, pp, up_bc, True, x.data_ptr(), up.data_ptr(), B, stream())
+    Pm = int(np.prod([int(v) for v in p], dtype=object))
+    pqp.mod_mul_scalar(up.data_ptr(), [Pm % m for m in q + p], up.data_ptr(), B, stream())
+    out = torch.empty_like(x)
+    H.approx_mod_down(pq, pp, down_bc, T["pinv_modq"], t, up.data_ptr(), out.data_ptr(), B, stream())
+    torch.cuda.synchronize()
+    assert torch.equal(out, x)
+
+
+@pytest.mark.parametrize("om,nm", [(1152921504606584833, 1152921504598720513), (97, 1152921504606584833),
+                                   (1152921504606584833, 65537), (1 << 40, 12289)])
+def test_switch_modulus(hip, om, nm):
+    H, ctx = hip
+    import torch
+
+    rng = np.random.default_rng(om % 1000)
+    v = rng.integers(0, om, size=4099, dtype=np.uint64)
+    v[:6] = [0, 1, om // 2, om // 2 + 1, om - 1, om - 2]
+    x = dev(v)
+    y = torch.empty_like(x)
+    H.switch_modulus(ctx, x.data_ptr(), y.data_ptr(), v.size, om, nm, stream())
+    assert np.array_equal(host(y), K.switch_modulus(v, om, nm))
+
+
+@pytest.mark.parametrize("log_n", [3, 10, 16])
+@pytest.mark.parametrize("eval_form", [True, False])
+def test_automorphism(hip, log_n, eval_form):
+    H, ctx = hip
+    import torch
+
+    n = 1 << log_n
+    q, r = O.moduli_chain(log_n, 2)
+    plan = H.NTTPlan(ctx, log_n, q, r)
+    rng = np.random.default_rng(log_n)
+    x = _uniform(rng, 2, q, n)
+    x[0, 0, :4] = 0
+    ks_ = (3, 5, 2 * n - 1, 25) if log_n <= 10 else (5, 2 * n - 1)
+    for k in ks_:
+        y = torch.empty((2, 2, n), dtype=torch.int64, device="cuda")
+        dx = dev(x)
+        plan.automorphism(k, eval_form, dx.data_ptr(), y.data_ptr(), 2, stream())
+        got = host(y)
+        if log_n <= 10:
+            for b in range(2):
+                for t in range(2):
+                    assert np.array_equal(got[b, t], K.automorphism(x[b, t], k, eval_form, q[t])), (k, b, t)
+        else:  # full size: permutation property against the closed form
+            j = np.arange(n, dtype=np.uint64)
+            if eval_form:
+                rev = lambda v: np.array([int(format(int(a), f"0{log_n}b")[::-1], 2) for a in v], np.uint64)
+                src = rev(((np.uint64(k) * (2 * j + 1)) % np.uint64(2 * n)) >> np.uint64(1))
+                assert np.array_equal(got[:, :, rev(j)], x[:, :, src])
+            else:
+                jk = (j * np.uint64(k)) % np.uint64(2 * n)
+                neg = (jk >> np.uint64(log_n)) & np.uint64(1)
+                for t in range(2):
+                    exp = np.where(neg == 1, np.uint64(q[t]) - x[:, t], x[:, t])
+                    assert np.array_equal(got[:, t, jk % np.uint64(n)], exp)
+    with pytest.raises(H.MathError):
+        plan.automorphism(4, eval_form, dx.data_ptr(), y.data_ptr(), 2, stream())
+
+
+def test_mod_down_t_after_plain_same_objects(hip):
+    """ModDown with t = 0 and then t > 0 on the same plans / converter, N = 2^12
+    (the C++ adapter test's sequence)."""
+    H, ctx = hip
+    import torch
+
+    log_n, sq, sp = 12, 4, 2
+    n = 1 << log_n
+    q, rq, p, rp = _bases(log_n, sq, sp)
+    pq, pp = H.NTTPlan(ctx, log_n, q, rq), H.NTTPlan(ctx, log_n, p, rp)
+    pqp = H.NTTPlan(ctx, log_n, q + p, rq + rp)
+    up_bc, down_bc = _converter(H, ctx, log_n, q, p), _converter(H, ctx, log_n, p, q)
+    T = K.moddown_tables(q, p)
+    B = 2
+    rng = np.random.default_rng(1)
+    x = _uniform(rng, B, q, n)
+    dx = dev(x)
+    up = torch.empty((B, sq + sp, n), dtype=torch.int64, device="cuda")
+    H.approx_mod_up(pq, pp, up_bc, True, dx.data_ptr(), up.data_ptr(), B, stream())
+    Pm = int(np.prod([int(v) for v in p], dtype=object))
+    for t in (0, 65537, 0, 3):
+        scaled = torch.empty_like(up)
+        pqp.mod_mul_scalar(up.data_ptr(), [Pm % m for m in q + p], scaled.data_ptr(), B, stream())
+        out = torch.zeros((B, sq, n), dtype=torch.int64, device="cuda")
+        H.approx_mod_down(pq, pp, down_bc, T["pinv_modq"], t, scaled.data_ptr(), out.data_ptr(), B, stream())
+        assert np.array_equal(host(out), x), t

@@ -70,7 +70,8 @@ def test_kat_transform(hip):
     assert host(y).reshape(-1).tolist() == k["expected"]
     # same through the fused pipeline (b = NTT(a))
     c = dev(np.zeros_like(a))
-    plan.ntt_mul_intt(dev(a).data_ptr(), x.data_ptr(), c.data_ptr(), 1, stream())
+    da = dev(a)  # referenced until the stream has consumed it
+    plan.ntt_mul_intt(da.data_ptr(), x.data_ptr(), c.data_ptr(), 1, stream())
     assert host(c).reshape(-1).tolist() == k["expected"]
 
 
@@ -251,7 +252,8 @@ def test_base_conversion_config5_shape(hip, O):
     x = O.uniform_dcrt(1, sq, n, q, 31)
     bc = H.BaseConverter(ctx, log_n, q, p, [int(v) for v in pre["qhinv"]], [int(v) for v in pre["qhmodp"]])
     out = torch.zeros((1, sp, n), dtype=torch.int64, device="cuda")
-    bc.switch(dev(x).data_ptr(), out.data_ptr(), 1, stream())
+    dx = dev(x)
+    bc.switch(dx.data_ptr(), out.data_ptr(), 1, stream())
     assert np.array_equal(host(out)[0], O.approx_switch_crt_basis(x[0], q, p, pre))
 
 

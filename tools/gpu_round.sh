@@ -4,7 +4,7 @@
 # else (abort, segfault, timeout) stops the session.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
-timeout -k 10 ${PYTEST_TIMEOUT:-500} python -m pytest tests -m gpu -q --timeout 240 ${PYTEST_ARGS} > gpurun_out/pytest_gpu.txt 2>&1
+PYTHONUNBUFFERED=1 timeout -k 10 ${PYTEST_TIMEOUT:-500} python -m pytest ${PYTEST_PATHS:-tests} -m gpu -q -rf --timeout 240 --timeout-method=thread ${PYTEST_ARGS} > gpurun_out/pytest_gpu.txt 2>&1
 rc=$?
 tail -25 gpurun_out/pytest_gpu.txt
 echo "pytest rc=$rc"

@@ -60,7 +60,10 @@ struct BconvArgs {
     const u64* qhmodp;    // [sizeQ][sizeP]
     const u64* pv;        // [sizeP]
     const u64* pmu;       // [sizeP][2]  (mu_lo, mu_hi) = floor(2^128 / p)
+    u64 in_stride;        // words between batch entries of x   (sizeQ * N when dense)
+    u64 out_stride;       // words between batch entries of out (sizeP * N when dense)
     u32 log_n, size_q, size_p;
+    u32 gap_at, gap;      // output tower j >= gap_at is written at j + gap (key-switch digit slot)
 };
 
 template <int PT>
@@ -70,8 +73,8 @@ __global__ __launch_bounds__(256) void k_bconv(BconvArgs A, const u64* __restric
     const u64 gid = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (gid >= (u64)batch * N) return;
     const u32 b = (u32)(gid >> A.log_n), ri = (u32)(gid & (N - 1));
-    const u64* xb = x + (u64)b * A.size_q * N + ri;
-    u64* ob = out + (u64)b * A.size_p * N + ri;
+    const u64* xb = x + (u64)b * A.in_stride + ri;
+    u64* ob = out + (u64)b * A.out_stride + ri;
     for (u32 j0 = 0; j0 < A.size_p; j0 += PT) {
         u64 lo[PT], hi[PT];
 #pragma unroll
@@ -95,7 +98,8 @@ __global__ __launch_bounds__(256) void k_bconv(BconvArgs A, const u64* __restric
         for (int j = 0; j < PT; j++) {
             if (j < (int)jn) {
                 const u32 jj = j0 + j;
-                ob[(u64)jj * N] = barrett128(lo[j], hi[j], A.pv[jj], A.pmu[2 * jj], A.pmu[2 * jj + 1]);
+                const u32 jo = jj >= A.gap_at ? jj + A.gap : jj;
+                ob[(u64)jo * N] = barrett128(lo[j], hi[j], A.pv[jj], A.pmu[2 * jj], A.pmu[2 * jj + 1]);
             }
         }
     }

@@ -1,0 +1,103 @@
+// internal.hpp -- definitions shared by the translation units of the backend
+// (ofhe_hip.hip: context, plans, NTT, element-wise ops, base conversion;
+// keyswitch.hip: ApproxModUp / ApproxModDown / hybrid key switching).
+// Not part of the C ABI.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <atomic>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/ofhe_hip.h"
+#include "eltwise_kernels.hpp"
+
+namespace ofhe {
+typedef unsigned __int128 u128;
+
+int fail(int code, const std::string& msg);
+int post_launch();
+
+#define HIPCHK(call)                                                                        \
+    do {                                                                                    \
+        hipError_t e_ = (call);                                                             \
+        if (e_ != hipSuccess)                                                               \
+            return ofhe::fail(OFHE_ERR_HIP, std::string(#call) + ": " + hipGetErrorString(e_)); \
+    } while (0)
+#define RCCHK(call)            \
+    do {                       \
+        int rc_ = (call);      \
+        if (rc_) return rc_;   \
+    } while (0)
+
+// host-side number theory for table construction (setup, not timed)
+inline u64 mulmod(u64 a, u64 b, u64 q) { return (u64)(((u128)a * b) % q); }
+inline u64 powmod(u64 b, u64 e, u64 q) {
+    u64 r = 1 % q;
+    b %= q;
+    while (e) {
+        if (e & 1) r = mulmod(r, b, q);
+        b = mulmod(b, b, q);
+        e >>= 1;
+    }
+    return r;
+}
+inline u64 invmod(u64 a, u64 q) { return powmod(a, q - 2, q); }  // q prime
+inline u64 shoup_pre(u64 w, u64 q) { return (u64)(((u128)w << 64) / q); }
+inline unsigned msb64(u64 x) { return x ? 64u - (unsigned)__builtin_clzll(x) : 0u; }
+inline u32 bitrev(u32 x, unsigned bits) {
+    u32 r = 0;
+    for (unsigned i = 0; i < bits; i++) {
+        r = (r << 1) | (x & 1);
+        x >>= 1;
+    }
+    return r;
+}
+
+// NULL selects the device's default (null) stream, as the header documents;
+// callers that want overlap pass their own stream (e.g. torch's).
+inline hipStream_t pick(void* stream) { return (hipStream_t)stream; }
+
+// NTT / INTT of plan towers [t0, t0 + count) over `batch` entries; src and dst
+// point at tower t0 of batch entry 0 and advance by sstride / dstride words
+// per entry.  src may equal dst (in place).
+int plan_ntt_range(ofhe_plan_t p, bool inverse, u32 t0, u32 count, const u64* src, u64* dst, u64 sstride,
+                   u64 dstride, u32 batch, hipStream_t s);
+
+// ApproxSwitchCRTBasis launch (strides and output gap from A)
+int bconv_run(const BconvArgs& A, const u64* x, u64* out, u32 batch, hipStream_t s);
+
+}  // namespace ofhe
+
+struct ofhe_ctx_s {
+    int device = 0;
+    std::atomic<int> live{1};
+};
+
+struct ofhe_plan_s {
+    ofhe_ctx_t ctx = nullptr;
+    ofhe::u32 log_n = 0, towers = 0;
+    // device
+    ofhe::TowerConst* d_tc = nullptr;
+    ofhe::u64* d_tw = nullptr;
+    ofhe::u64* d_itw = nullptr;
+    ofhe::u64* d_itwn = nullptr;
+    // host copies (for ofhe_hip_plan_tables and scalar prep)
+    std::vector<ofhe::u64> q, psi, tab, tab_pre, itab, itab_pre, ninv;
+    ofhe::u64* d_scal = nullptr;  // scratch for per-tower scalars (modmul_scalar)
+    std::mutex scal_mu;
+    // pipeline tuning (ofhe_hip_plan_tune): batch entries per chunk (0 = all)
+    // and internal streams the chunks alternate over (1 = caller's stream).
+    ofhe::u32 chunk_batch = 0, nstreams = 1;
+    bool spq = false;     // every modulus is 2^L - d with d < 2^32 (special-prime kernels)
+    bool split8 = false;  // log_n == 16: 8 column stages + 8 block stages (k_tcols + k_block<.,.,2>)
+    hipStream_t st[2] = {nullptr, nullptr};
+    hipEvent_t ev_fork = nullptr, ev_join[2] = {nullptr, nullptr};
+};
+
+struct ofhe_bconv_s {
+    ofhe_ctx_t ctx = nullptr;
+    ofhe::BconvArgs args{};
+    ofhe::u64* d_mem = nullptr;
+};

@@ -1,0 +1,493 @@
+// keyswitch.hip -- ApproxModUp / ApproxModDown and HYBRID key switching on
+// gfx950, composed from the NTT, base-conversion and element kernels.
+//
+// Reference call stacks restated here (one launch per step covers the whole
+// batch; the reference loops over towers with OpenMP):
+//   DCRTPolyImpl::ApproxModUp    dcrtpoly-impl.h:1085-1131
+//   DCRTPolyImpl::ApproxModDown  dcrtpoly-impl.h:1134-1175
+//   KeySwitchHYBRID::EvalKeySwitchPrecomputeCore  keyswitch-hybrid.cpp:330-412
+//   KeySwitchHYBRID::EvalFastKeySwitchCoreExt     keyswitch-hybrid.cpp:438-482
+//   KeySwitchHYBRID::EvalFastKeySwitchCore        keyswitch-hybrid.cpp:414-436
+// CRT tables follow CryptoParametersRNS::PrecomputeCRTTables
+// (rns-cryptoparameters.cpp:72-345).  The reference builds them with
+// BigInteger quotients (Q/q_i) and reductions; every table entry is a residue
+// of a product of the moduli, so it is computed here as that product reduced
+// modulo the target prime -- the same integer.
+#include <map>
+#include <new>
+
+#include "internal.hpp"
+#include "ks_kernels.hpp"
+
+using namespace ofhe;
+
+namespace {
+
+// prod_{k != skip} ms[k] mod m
+u64 prod_mod(const u64* ms, u32 n, u32 skip, u64 m) {
+    u64 r = 1 % m;
+    for (u32 k = 0; k < n; k++)
+        if (k != skip) r = mulmod(r, ms[k] % m, m);
+    return r;
+}
+
+u32 grid_for(u64 items) {
+    u64 b = (items + 255) / 256;
+    if (b > 256 * 16) b = 256 * 16;
+    return (u32)(b ? b : 1);
+}
+
+TowerScalar scalar_of(u64 q, u64 s) {
+    s %= q;
+    return TowerScalar{q, s, shoup_pre(s, q)};
+}
+
+int scale_towers(const TowerScalar* d, const u64* x, u64* out, u64 xs, u64 os, u32 batch, u32 towers, u32 log_n,
+                 hipStream_t s) {
+    const u64 npairs = ((u64)batch * towers << log_n) / 2;
+    hipLaunchKernelGGL(k_scale_towers, dim3(grid_for(npairs)), dim3(256), 0, s, d, x, out, xs, os, npairs, log_n,
+                       towers);
+    return post_launch();
+}
+
+int sub_scale(const TowerScalar* d, const u64* x, const u64* y, u64* out, u64 xs, u64 ys, u64 os, u32 batch,
+              u32 towers, u32 log_n, hipStream_t s) {
+    const u64 npairs = ((u64)batch * towers << log_n) / 2;
+    hipLaunchKernelGGL(k_sub_scale, dim3(grid_for(npairs)), dim3(256), 0, s, d, x, y, out, xs, ys, os, npairs,
+                       log_n, towers);
+    return post_launch();
+}
+
+// Stream-ordered scratch: freed on the stream when the owner goes out of scope.
+struct Scratch {
+    void* p = nullptr;
+    hipStream_t s = nullptr;
+    int alloc(size_t bytes, hipStream_t st) {
+        s = st;
+        hipError_t e = hipMallocAsync(&p, bytes ? bytes : 8, st);
+        if (e != hipSuccess) return fail(OFHE_ERR_NOMEM, std::string("scratch: ") + hipGetErrorString(e));
+        return OFHE_OK;
+    }
+    u64* w() const { return (u64*)p; }
+    ~Scratch() {
+        if (p) (void)hipFreeAsync(p, s);
+    }
+};
+
+// small constant table staged for one call (host memory must outlive the copy)
+int stage_table(Scratch& sc, const void* host, size_t bytes, hipStream_t s) {
+    RCCHK(sc.alloc(bytes, s));
+    HIPCHK(hipMemcpyAsync(sc.p, host, bytes, hipMemcpyHostToDevice, s));
+    HIPCHK(hipStreamSynchronize(s));
+    return OFHE_OK;
+}
+
+int copy_rows(u64* dst, u64 dstride, const u64* src, u64 sstride, u64 words, u32 rows, hipStream_t s) {
+    if (!words || !rows) return OFHE_OK;
+    HIPCHK(hipMemcpy2DAsync(dst, dstride * 8, src, sstride * 8, words * 8, rows, hipMemcpyDeviceToDevice, s));
+    return OFHE_OK;
+}
+
+// ApproxModDown core shared by the generic entry point and the key-switch
+// engine.  x: [batch][Q+P] (xstride), the P part at x + Q*N; plan towers
+// pq0.. for Q and pp0.. for P (both in `plan_q` / `plan_p`).
+struct ModDownArgs {
+    ofhe_plan_t plan_q, plan_p;
+    u32 q0, p0, size_q, size_p;
+    BconvArgs bconv;               // P -> Q
+    const TowerScalar* pinv;       // [size_q]
+    const TowerScalar* tinv_p;     // [size_p] or NULL (t = 0)
+    const TowerScalar* t_q;        // [size_q] or NULL
+};
+
+int mod_down_run(const ModDownArgs& A, const u64* x, u64 xstride, u64* out, u64 ostride, u32 batch, hipStream_t s) {
+    const u32 log_n = A.plan_q->log_n;
+    const u64 N = 1ull << log_n;
+    Scratch sp, sq;
+    RCCHK(sp.alloc((size_t)batch * A.size_p * N * 8, s));
+    RCCHK(sq.alloc((size_t)batch * A.size_q * N * 8, s));
+    const u64 ps = A.size_p * N, qs = A.size_q * N;
+    // partP: P towers to coefficient form (dcrtpoly-impl.h:1147-1153)
+    RCCHK(plan_ntt_range(A.plan_p, true, A.p0, A.size_p, x + qs, sp.w(), xstride, ps, batch, s));
+    if (A.tinv_p) RCCHK(scale_towers(A.tinv_p, sp.w(), sp.w(), ps, ps, batch, A.size_p, log_n, s));
+    // partPSwitchedToQ (1156-1157)
+    BconvArgs B = A.bconv;
+    B.in_stride = ps;
+    B.out_stride = qs;
+    B.gap_at = A.size_q;
+    B.gap = 0;
+    RCCHK(bconv_run(B, sp.w(), sq.w(), batch, s));
+    if (A.t_q) RCCHK(scale_towers(A.t_q, sq.w(), sq.w(), qs, qs, batch, A.size_q, log_n, s));
+    RCCHK(plan_ntt_range(A.plan_q, false, A.q0, A.size_q, sq.w(), sq.w(), qs, qs, batch, s));
+    // ans_i = (x_i - switched_i) * PInvModq_i (1167-1173)
+    return sub_scale(A.pinv, x, sq.w(), out, xstride, qs, ostride, batch, A.size_q, log_n, s);
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// Generic ApproxModUp / ApproxModDown
+// ---------------------------------------------------------------------------
+int ofhe_hip_approx_mod_up(ofhe_plan_t pq, ofhe_plan_t pp, ofhe_bconv_t bc, int eval_form, const uint64_t* x,
+                           uint64_t* out, uint32_t batch, void* stream) {
+    if (!pq || !pp || !bc || !pq->ctx || !pp->ctx || !bc->ctx) return fail(OFHE_ERR_STATE, "NULL or destroyed object");
+    if (!x || !out || batch == 0) return fail(OFHE_ERR_ARG, "bad data argument");
+    if (pq->log_n != pp->log_n || bc->args.log_n != pq->log_n) return fail(OFHE_ERR_ARG, "ring dimensions differ");
+    if (bc->args.size_q != pq->towers || bc->args.size_p != pp->towers)
+        return fail(OFHE_ERR_ARG, "base converter does not map plan_q's towers to plan_p's");
+    HIPCHK(hipSetDevice(pq->ctx->device));
+    hipStream_t s = pick(stream);
+    const u64 N = 1ull << pq->log_n, Q = pq->towers, P = pp->towers, qp = (Q + P) * N;
+    BconvArgs B = bc->args;
+    B.out_stride = qp;
+    if (eval_form) {
+        // coefficient copy of x (SetFormat(COEFFICIENT), 1097-1100) into the Q slots
+        RCCHK(plan_ntt_range(pq, true, 0, (u32)Q, x, out, Q * N, qp, batch, s));
+        B.in_stride = qp;
+        RCCHK(bconv_run(B, out, out + Q * N, batch, s));
+    } else {
+        B.in_stride = Q * N;
+        RCCHK(bconv_run(B, x, out + Q * N, batch, s));
+    }
+    // P towers to evaluation form (1112-1116)
+    RCCHK(plan_ntt_range(pp, false, 0, (u32)P, out + Q * N, out + Q * N, qp, qp, batch, s));
+    // Q towers: the stored evaluation input, or its NTT (1119-1127)
+    if (eval_form) return copy_rows(out, qp, x, Q * N, Q * N, batch, s);
+    return plan_ntt_range(pq, false, 0, (u32)Q, x, out, Q * N, qp, batch, s);
+}
+
+int ofhe_hip_approx_mod_down(ofhe_plan_t pq, ofhe_plan_t pp, ofhe_bconv_t bc, const uint64_t* p_inv_modq,
+                             uint64_t t, const uint64_t* x, uint64_t* out, uint32_t batch, void* stream) {
+    if (!pq || !pp || !bc || !pq->ctx || !pp->ctx || !bc->ctx) return fail(OFHE_ERR_STATE, "NULL or destroyed object");
+    if (!x || !out || !p_inv_modq || batch == 0) return fail(OFHE_ERR_ARG, "bad data argument");
+    if (pq->log_n != pp->log_n || bc->args.log_n != pq->log_n) return fail(OFHE_ERR_ARG, "ring dimensions differ");
+    if (bc->args.size_q != pp->towers || bc->args.size_p != pq->towers)
+        return fail(OFHE_ERR_ARG, "base converter does not map plan_p's towers to plan_q's");
+    HIPCHK(hipSetDevice(pq->ctx->device));
+    hipStream_t s = pick(stream);
+    const u32 Q = pq->towers, P = pp->towers;
+    std::vector<TowerScalar> tab(Q + (t ? P + Q : 0));
+    for (u32 i = 0; i < Q; i++) tab[i] = scalar_of(pq->q[i], p_inv_modq[i]);
+    if (t) {
+        for (u32 j = 0; j < P; j++) tab[Q + j] = scalar_of(pp->q[j], invmod(t % pp->q[j], pp->q[j]));  // tInvModp
+        for (u32 i = 0; i < Q; i++) tab[Q + P + i] = scalar_of(pq->q[i], t);                          // t mod q_i
+    }
+    Scratch dt;
+    RCCHK(stage_table(dt, tab.data(), tab.size() * sizeof(TowerScalar), s));
+    const TowerScalar* d = (const TowerScalar*)dt.p;
+    ModDownArgs A{pq, pp, 0, 0, Q, P, bc->args, d, t ? d + Q : nullptr, t ? d + Q + P : nullptr};
+    const u64 N = 1ull << pq->log_n;
+    return mod_down_run(A, x, (u64)(Q + P) * N, out, (u64)Q * N, batch, s);
+}
+
+// ---------------------------------------------------------------------------
+// HYBRID key switching
+// ---------------------------------------------------------------------------
+struct KsLevel {
+    u32 size_ql = 0, beta = 0;
+    std::vector<u32> start, cnt;        // digit j = towers [start, start + cnt)
+    std::vector<ofhe_bconv_t> up;       // digit j -> its complement basis (Ql \ digit) | P
+    ofhe_bconv_t down = nullptr;        // P -> Ql
+    KsTower* d_tow = nullptr;           // [size_ql + size_p]
+    TowerScalar* d_pinv = nullptr;      // [size_ql] P^-1 mod q_i
+    std::map<u64, TowerScalar*> tscale; // t -> [size_p] t^-1 mod p_j, then [size_ql] t mod q_i
+};
+
+struct ofhe_ks_s {
+    ofhe_ctx_t ctx = nullptr;
+    u32 log_n = 0, size_q = 0, size_p = 0, num_part_q = 0, alpha = 0;
+    std::vector<u64> q, p;
+    ofhe_plan_t plan = nullptr;  // towers q[0..size_q) then p[0..size_p)
+    std::mutex mu;
+    std::map<u32, KsLevel*> levels;
+};
+
+static void level_free(KsLevel* L) {
+    if (!L) return;
+    for (auto b : L->up) ofhe_hip_bconv_destroy(b);
+    if (L->down) ofhe_hip_bconv_destroy(L->down);
+    (void)hipFree(L->d_tow);
+    (void)hipFree(L->d_pinv);
+    for (auto& kv : L->tscale) (void)hipFree(kv.second);
+    delete L;
+}
+
+int ofhe_hip_ks_create(ofhe_ctx_t ctx, uint32_t log_n, uint32_t size_q, const uint64_t* q, const uint64_t* psi_q,
+                       uint32_t size_p, const uint64_t* p, const uint64_t* psi_p, uint32_t num_part_q,
+                       ofhe_ks_t* out) {
+    if (!ctx || !q || !psi_q || !p || !psi_p || !out) return fail(OFHE_ERR_ARG, "NULL argument");
+    if (size_q < 1 || size_p < 1 || size_q + size_p > 256) return fail(OFHE_ERR_ARG, "size_q + size_p must be in [2, 256]");
+    if (num_part_q < 1 || num_part_q > size_q) return fail(OFHE_ERR_ARG, "num_part_q must be in [1, size_q]");
+    const u32 alpha = (size_q + num_part_q - 1) / num_part_q;
+    // rns-cryptoparameters.cpp:75-83
+    if ((int32_t)(size_q - alpha * (num_part_q - 1)) <= 0)
+        return fail(OFHE_ERR_ARG, "HYBRID key switching: can't distribute " + std::to_string(size_q) + " towers into " +
+                                      std::to_string(num_part_q) + " digits");
+    for (u32 j = 0; j < size_p; j++)
+        for (u32 i = 0; i < size_q; i++)
+            if (p[j] == q[i]) return fail(OFHE_ERR_ARG, "P and Q moduli must be distinct");
+    std::vector<u64> mq(q, q + size_q), mp(p, p + size_p), all(mq), roots(psi_q, psi_q + size_q);
+    all.insert(all.end(), mp.begin(), mp.end());
+    roots.insert(roots.end(), psi_p, psi_p + size_p);
+    ofhe_plan_t plan = nullptr;
+    RCCHK(ofhe_hip_plan_create(ctx, log_n, size_q + size_p, all.data(), roots.data(), &plan));
+    ofhe_ks_s* k = new (std::nothrow) ofhe_ks_s();
+    if (!k) {
+        ofhe_hip_plan_destroy(plan);
+        return fail(OFHE_ERR_NOMEM, "key-switch allocation failed");
+    }
+    k->ctx = ctx;
+    k->log_n = log_n;
+    k->size_q = size_q;
+    k->size_p = size_p;
+    k->num_part_q = num_part_q;
+    k->alpha = alpha;
+    k->q = mq;
+    k->p = mp;
+    k->plan = plan;
+    *out = k;
+    return OFHE_OK;
+}
+
+int ofhe_hip_ks_destroy(ofhe_ks_t k) {
+    if (!k) return fail(OFHE_ERR_ARG, "key switch is NULL");
+    if (k->ctx) (void)hipSetDevice(k->ctx->device);
+    (void)hipDeviceSynchronize();
+    for (auto& kv : k->levels) level_free(kv.second);
+    if (k->plan) ofhe_hip_plan_destroy(k->plan);
+    delete k;
+    return OFHE_OK;
+}
+
+int ofhe_hip_ks_digits(ofhe_ks_t k, uint32_t size_ql, uint32_t* alpha, uint32_t* beta) {
+    if (!k || !k->ctx) return fail(OFHE_ERR_STATE, "key switch is NULL or destroyed");
+    if (size_ql < 1 || size_ql > k->size_q) return fail(OFHE_ERR_ARG, "size_ql must be in [1, size_q]");
+    // keyswitch-hybrid.cpp:341-345
+    u32 b = (size_ql + k->alpha - 1) / k->alpha;
+    if (b > k->num_part_q) b = k->num_part_q;
+    if (alpha) *alpha = k->alpha;
+    if (beta) *beta = b;
+    return OFHE_OK;
+}
+
+// Tables of one level l = size_ql - 1 (built once, kept resident).
+static int level_get(ofhe_ks_t k, u32 size_ql, KsLevel** out) {
+    std::lock_guard<std::mutex> lk(k->mu);
+    auto it = k->levels.find(size_ql);
+    if (it != k->levels.end()) {
+        *out = it->second;
+        return OFHE_OK;
+    }
+    u32 beta = 0;
+    RCCHK(ofhe_hip_ks_digits(k, size_ql, nullptr, &beta));
+    KsLevel* L = new (std::nothrow) KsLevel();
+    if (!L) return fail(OFHE_ERR_NOMEM, "level allocation failed");
+    const u32 P = k->size_p, l = size_ql;
+    L->beta = beta;
+    L->size_ql = l;
+    int rc = OFHE_OK;
+    for (u32 j = 0; j < L->beta && rc == OFHE_OK; j++) {
+        // digit j (keyswitch-hybrid.cpp:352-378) and its complement
+        // (m_paramsComplPartQ, rns-cryptoparameters.cpp:238-287)
+        const u32 st = j * k->alpha, n = std::min(k->alpha, l - st);
+        L->start.push_back(st);
+        L->cnt.push_back(n);
+        const u64* dq = k->q.data() + st;
+        std::vector<u64> compl_;
+        for (u32 i = 0; i < l; i++)
+            if (i < st || i >= st + n) compl_.push_back(k->q[i]);
+        compl_.insert(compl_.end(), k->p.begin(), k->p.end());
+        const u32 C = (u32)compl_.size();
+        std::vector<u64> hinv(n), hmod((size_t)n * C);
+        for (u32 i = 0; i < n; i++) {
+            // m_PartQlHatInvModq[j][n-1][i] (rns-cryptoparameters.cpp:289-312)
+            hinv[i] = invmod(prod_mod(dq, n, i, dq[i]), dq[i]);
+            // m_PartQlHatModp[l][j][i][c] (314-341)
+            for (u32 c = 0; c < C; c++) hmod[(size_t)i * C + c] = prod_mod(dq, n, i, compl_[c]);
+        }
+        ofhe_bconv_t b = nullptr;
+        rc = ofhe_hip_bconv_create(k->ctx, k->log_n, n, C, dq, compl_.data(), hinv.data(), hmod.data(), &b);
+        if (rc == OFHE_OK) L->up.push_back(b);
+    }
+    if (rc == OFHE_OK) {
+        // ApproxModDown tables: PHatInvModp, PHatModq, PInvModq (172-215)
+        std::vector<u64> hinv(P), hmod((size_t)P * l);
+        for (u32 j = 0; j < P; j++) {
+            hinv[j] = invmod(prod_mod(k->p.data(), P, j, k->p[j]), k->p[j]);
+            for (u32 i = 0; i < l; i++) hmod[(size_t)j * l + i] = prod_mod(k->p.data(), P, j, k->q[i]);
+        }
+        rc = ofhe_hip_bconv_create(k->ctx, k->log_n, P, l, k->p.data(), k->q.data(), hinv.data(), hmod.data(),
+                                   &L->down);
+    }
+    if (rc == OFHE_OK) {
+        const u64 N = 1ull << k->log_n;
+        std::vector<KsTower> tow(l + P);
+        for (u32 i = 0; i < l + P; i++) {
+            const bool isq = i < l;
+            const u64 m = isq ? k->q[i] : k->p[i - l];
+            const u128 mu = (~(u128)0) / m;
+            tow[i] = KsTower{m, (u64)mu, (u64)(mu >> 64), (isq ? i : k->size_q + i - l) * N};
+        }
+        std::vector<TowerScalar> pinv(l);
+        for (u32 i = 0; i < l; i++)
+            pinv[i] = scalar_of(k->q[i], invmod(prod_mod(k->p.data(), P, P, k->q[i]), k->q[i]));
+        hipError_t e = hipSetDevice(k->ctx->device);
+        if (e == hipSuccess) e = hipMalloc(&L->d_tow, sizeof(KsTower) * tow.size());
+        if (e == hipSuccess) e = hipMalloc(&L->d_pinv, sizeof(TowerScalar) * pinv.size());
+        if (e == hipSuccess) e = hipMemcpy(L->d_tow, tow.data(), sizeof(KsTower) * tow.size(), hipMemcpyHostToDevice);
+        if (e == hipSuccess)
+            e = hipMemcpy(L->d_pinv, pinv.data(), sizeof(TowerScalar) * pinv.size(), hipMemcpyHostToDevice);
+        if (e != hipSuccess) rc = fail(OFHE_ERR_HIP, std::string("level upload: ") + hipGetErrorString(e));
+    }
+    if (rc != OFHE_OK) {
+        level_free(L);
+        return rc;
+    }
+    k->levels[size_ql] = L;
+    *out = L;
+    return OFHE_OK;
+}
+
+static int level_t_tables(ofhe_ks_t k, KsLevel* L, u64 t, const TowerScalar** out) {
+    std::lock_guard<std::mutex> lk(k->mu);
+    auto it = L->tscale.find(t);
+    if (it != L->tscale.end()) {
+        *out = it->second;
+        return OFHE_OK;
+    }
+    const u32 P = k->size_p, l = L->size_ql;
+    std::vector<TowerScalar> tab(P + l);
+    for (u32 j = 0; j < P; j++) tab[j] = scalar_of(k->p[j], invmod(t % k->p[j], k->p[j]));
+    for (u32 i = 0; i < l; i++) tab[P + i] = scalar_of(k->q[i], t);
+    TowerScalar* d = nullptr;
+    HIPCHK(hipMalloc(&d, sizeof(TowerScalar) * tab.size()));
+    hipError_t e = hipMemcpy(d, tab.data(), sizeof(TowerScalar) * tab.size(), hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+        (void)hipFree(d);
+        return fail(OFHE_ERR_HIP, std::string("t tables: ") + hipGetErrorString(e));
+    }
+    L->tscale[t] = d;
+    *out = d;
+    return OFHE_OK;
+}
+
+static int ks_check(ofhe_ks_t k, u32 size_ql, u32 batch) {
+    if (!k || !k->ctx) return fail(OFHE_ERR_STATE, "key switch is NULL or destroyed");
+    if (size_ql < 1 || size_ql > k->size_q) return fail(OFHE_ERR_ARG, "size_ql must be in [1, size_q]");
+    if (batch == 0) return fail(OFHE_ERR_ARG, "batch must be >= 1");
+    HIPCHK(hipSetDevice(k->ctx->device));
+    return OFHE_OK;
+}
+
+int ofhe_hip_ks_precompute(ofhe_ks_t k, uint32_t size_ql, const uint64_t* c, uint64_t* digits, uint32_t batch,
+                           void* stream) {
+    RCCHK(ks_check(k, size_ql, batch));
+    if (!c || !digits) return fail(OFHE_ERR_ARG, "NULL data pointer");
+    KsLevel* L = nullptr;
+    RCCHK(level_get(k, size_ql, &L));
+    hipStream_t s = pick(stream);
+    const u64 N = 1ull << k->log_n, l = size_ql, P = k->size_p, poly = (l + P) * N, ds = L->beta * poly;
+    for (u32 j = 0; j < L->beta; j++) {
+        const u32 st = L->start[j], n = L->cnt[j];
+        u64* slot = digits + j * poly;
+        // partsCt[j] in coefficient form (keyswitch-hybrid.cpp:384-385)
+        RCCHK(plan_ntt_range(k->plan, true, st, n, c + st * N, slot + st * N, l * N, ds, batch, s));
+        // ApproxSwitchCRTBasis to the complement, written around the digit slot (388-406)
+        BconvArgs B = L->up[j]->args;
+        B.in_stride = B.out_stride = ds;
+        B.gap_at = st;
+        B.gap = n;
+        RCCHK(bconv_run(B, slot + st * N, slot, batch, s));
+        // complement towers to evaluation form (394)
+        RCCHK(plan_ntt_range(k->plan, false, 0, st, slot, slot, ds, ds, batch, s));
+        RCCHK(plan_ntt_range(k->plan, false, st + n, (u32)l - st - n, slot + (st + n) * N, slot + (st + n) * N, ds,
+                             ds, batch, s));
+        RCCHK(plan_ntt_range(k->plan, false, k->size_q, (u32)P, slot + l * N, slot + l * N, ds, ds, batch, s));
+        // the digit's own towers stay as given (evaluation form, 402-404)
+        RCCHK(copy_rows(slot + st * N, ds, c + st * N, l * N, (u64)n * N, batch, s));
+    }
+    return OFHE_OK;
+}
+
+int ofhe_hip_ks_fast_core_ext(ofhe_ks_t k, uint32_t size_ql, const uint64_t* digits, const uint64_t* key_b,
+                              const uint64_t* key_a, uint64_t* ct0, uint64_t* ct1, uint32_t batch, void* stream) {
+    RCCHK(ks_check(k, size_ql, batch));
+    if (!digits || !key_b || !key_a || !ct0 || !ct1) return fail(OFHE_ERR_ARG, "NULL data pointer");
+    KsLevel* L = nullptr;
+    RCCHK(level_get(k, size_ql, &L));
+    const u32 towers = size_ql + k->size_p;
+    const u64 npairs = ((u64)batch * towers << k->log_n) / 2;
+    const u64 key_stride = (u64)(k->size_q + k->size_p) << k->log_n;
+    hipLaunchKernelGGL(k_ks_inner, dim3(grid_for(npairs)), dim3(256), 0, pick(stream), L->d_tow, digits, key_b, key_a,
+                       ct0, ct1, key_stride, L->beta, npairs, k->log_n, towers);
+    return post_launch();
+}
+
+static int ks_mod_down_impl(ofhe_ks_t k, KsLevel* L, const u64* x, u64* out, u64 t, u32 batch, hipStream_t s) {
+    const TowerScalar* tt = nullptr;
+    if (t) RCCHK(level_t_tables(k, L, t, &tt));
+    const u32 l = L->size_ql, P = k->size_p;
+    ModDownArgs A{k->plan, k->plan, 0, k->size_q, l, P, L->down->args, L->d_pinv,
+                  tt ? tt : nullptr, tt ? tt + P : nullptr};
+    const u64 N = 1ull << k->log_n;
+    return mod_down_run(A, x, (u64)(l + P) * N, out, (u64)l * N, batch, s);
+}
+
+int ofhe_hip_ks_mod_down(ofhe_ks_t k, uint32_t size_ql, const uint64_t* x, uint64_t* out, uint64_t t, uint32_t batch,
+                         void* stream) {
+    RCCHK(ks_check(k, size_ql, batch));
+    if (!x || !out) return fail(OFHE_ERR_ARG, "NULL data pointer");
+    KsLevel* L = nullptr;
+    RCCHK(level_get(k, size_ql, &L));
+    return ks_mod_down_impl(k, L, x, out, t, batch, pick(stream));
+}
+
+int ofhe_hip_ks_core(ofhe_ks_t k, uint32_t size_ql, const uint64_t* c, const uint64_t* key_b, const uint64_t* key_a,
+                     uint64_t* out0, uint64_t* out1, uint64_t t, uint32_t batch, void* stream) {
+    RCCHK(ks_check(k, size_ql, batch));
+    if (!c || !key_b || !key_a || !out0 || !out1) return fail(OFHE_ERR_ARG, "NULL data pointer");
+    KsLevel* L = nullptr;
+    RCCHK(level_get(k, size_ql, &L));
+    hipStream_t s = pick(stream);
+    const u64 N = 1ull << k->log_n, poly = (u64)(size_ql + k->size_p) * N;
+    Scratch dg, ct;
+    RCCHK(dg.alloc((size_t)batch * L->beta * poly * 8, s));
+    RCCHK(ct.alloc((size_t)2 * batch * poly * 8, s));
+    u64* c0 = ct.w();
+    u64* c1 = ct.w() + (u64)batch * poly;
+    RCCHK(ofhe_hip_ks_precompute(k, size_ql, c, dg.w(), batch, s));
+    RCCHK(ofhe_hip_ks_fast_core_ext(k, size_ql, dg.w(), key_b, key_a, c0, c1, batch, s));
+    RCCHK(ks_mod_down_impl(k, L, c0, out0, t, batch, s));
+    return ks_mod_down_impl(k, L, c1, out1, t, batch, s);
+}
+
+// ---------------------------------------------------------------------------
+// Element maps
+// ---------------------------------------------------------------------------
+int ofhe_hip_switch_modulus(ofhe_ctx_t ctx, const uint64_t* src, uint64_t* dst, uint64_t n, uint64_t old_q,
+                            uint64_t new_q, void* stream) {
+    if (!ctx || ((!src || !dst) && n)) return fail(OFHE_ERR_ARG, "NULL argument");
+    if (old_q < 2 || new_q < 2) return fail(OFHE_ERR_ARG, "moduli must be >= 2");
+    if (!n) return OFHE_OK;
+    HIPCHK(hipSetDevice(ctx->device));
+    hipLaunchKernelGGL(k_switch_modulus, dim3(grid_for(n)), dim3(256), 0, pick(stream), src, dst, (u64)n, (u64)old_q,
+                       (u64)new_q);
+    return post_launch();
+}
+
+int ofhe_hip_automorphism(ofhe_plan_t p, uint32_t k, int eval_form, const uint64_t* src, uint64_t* dst,
+                          uint32_t batch, void* stream) {
+    if (!p || !p->ctx) return fail(OFHE_ERR_STATE, "plan is NULL or destroyed");
+    if (!src || !dst || batch == 0) return fail(OFHE_ERR_ARG, "bad data argument");
+    if (src == dst) return fail(OFHE_ERR_ARG, "automorphism is out of place (dst must not alias src)");
+    if (k % 2 == 0) return fail(OFHE_ERR_ARG, "Automorphism index not odd");  // poly-impl.h:333-334
+    HIPCHK(hipSetDevice(p->ctx->device));
+    const u64 total = (u64)batch * p->towers << p->log_n;
+    if (eval_form)
+        hipLaunchKernelGGL(k_automorphism<true>, dim3(grid_for(total)), dim3(256), 0, pick(stream), p->d_tc, src, dst,
+                           k, total, p->log_n, p->towers);
+    else
+        hipLaunchKernelGGL(k_automorphism<false>, dim3(grid_for(total)), dim3(256), 0, pick(stream), p->d_tc, src,
+                           dst, k, total, p->log_n, p->towers);
+    return post_launch();
+}

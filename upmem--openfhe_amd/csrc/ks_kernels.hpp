@@ -1,0 +1,158 @@
+// ks_kernels.hpp -- element kernels of ApproxModUp / ApproxModDown, the
+// HYBRID key-switching inner product, SwitchModulus and automorphisms.
+//
+// All are HBM streams over [batch][towers][N] data with explicit batch
+// strides (words), so they can address a tower range of a wider polynomial
+// (the Q part of a Q|P polynomial, one digit slot of the key-switch digits)
+// without copies.  Each thread handles two adjacent coefficients (16-byte
+// accesses); N >= 2 keeps pairs inside one tower.
+#pragma once
+#include "eltwise_kernels.hpp"
+
+namespace ofhe {
+
+// one scalar per tower: s and its Shoup precon for modulus q
+struct TowerScalar {
+    u64 q, s, sp;
+};
+
+// (pair index) -> (batch entry, tower, coefficient) for `towers` towers of N
+struct PairIndex {
+    u32 b, t, c;
+};
+__device__ __forceinline__ PairIndex pair_index(u64 i, u32 log_n, u32 towers) {
+    const u64 e = 2 * i;
+    const u64 row = e >> log_n;
+    return PairIndex{(u32)(row / towers), (u32)(row % towers), (u32)(e & ((1ull << log_n) - 1))};
+}
+
+// out = x * s_t mod q_t (NativeVectorT::ModMulEq(scalar), mubintvecnat.cpp:310-332)
+__global__ __launch_bounds__(256) void k_scale_towers(const TowerScalar* __restrict__ ts, const u64* x, u64* out,
+                                                      u64 xstride, u64 ostride, u64 npairs, u32 log_n,
+                                                      u32 towers) {
+    const u64 step = (u64)gridDim.x * blockDim.x;
+    for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < npairs; i += step) {
+        const PairIndex p = pair_index(i, log_n, towers);
+        const TowerScalar c = ts[p.t];
+        const u64 inner = ((u64)p.t << log_n) + p.c;
+        const ulonglong2 v = *reinterpret_cast<const ulonglong2*>(x + p.b * xstride + inner);
+        *reinterpret_cast<ulonglong2*>(out + p.b * ostride + inner) =
+            make_ulonglong2(shoup_canon(v.x, c.s, c.sp, c.q), shoup_canon(v.y, c.s, c.sp, c.q));
+    }
+}
+
+// out = (x - y mod q_t) * s_t mod q_t: the last step of ApproxModDown,
+// (m_vectors[i] - partPSwitchedToQ[i]) * PInvModq[i] (dcrtpoly-impl.h:1172).
+__global__ __launch_bounds__(256) void k_sub_scale(const TowerScalar* __restrict__ ts, const u64* x, const u64* y,
+                                                   u64* out, u64 xstride, u64 ystride, u64 ostride, u64 npairs,
+                                                   u32 log_n, u32 towers) {
+    const u64 step = (u64)gridDim.x * blockDim.x;
+    for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < npairs; i += step) {
+        const PairIndex p = pair_index(i, log_n, towers);
+        const TowerScalar c = ts[p.t];
+        const u64 inner = ((u64)p.t << log_n) + p.c;
+        const ulonglong2 a = *reinterpret_cast<const ulonglong2*>(x + p.b * xstride + inner);
+        const ulonglong2 b = *reinterpret_cast<const ulonglong2*>(y + p.b * ystride + inner);
+        const u64 d0 = a.x < b.x ? a.x + c.q - b.x : a.x - b.x;  // ModSubFastEq
+        const u64 d1 = a.y < b.y ? a.y + c.q - b.y : a.y - b.y;
+        *reinterpret_cast<ulonglong2*>(out + p.b * ostride + inner) =
+            make_ulonglong2(shoup_canon(d0, c.s, c.sp, c.q), shoup_canon(d1, c.s, c.sp, c.q));
+    }
+}
+
+// Tower of the extended basis Ql|P for the key-switch inner product.
+struct KsTower {
+    u64 m;             // modulus
+    u64 mu_lo, mu_hi;  // floor(2^128 / m)
+    u64 key_off;       // word offset of this tower inside one key polynomial (QP layout)
+};
+
+// EvalFastKeySwitchCoreExt (keyswitch-hybrid.cpp:452-478):
+//   ct0[i] = sum_j digits_j[i] * b_j[key(i)],  ct1[i] = sum_j digits_j[i] * a_j[key(i)]
+// The reference accumulates canonical ModMul / ModAdd terms; the sum of exact
+// 128-bit products reduced once by BarrettUint128ModUint64 is the same
+// canonical residue (beta <= 2^8 terms below 2^120 cannot overflow 128 bits).
+__global__ __launch_bounds__(256) void k_ks_inner(const KsTower* __restrict__ tw, const u64* __restrict__ digits,
+                                                  const u64* __restrict__ kb, const u64* __restrict__ ka,
+                                                  u64* __restrict__ ct0, u64* __restrict__ ct1, u64 key_stride,
+                                                  u32 beta, u64 npairs, u32 log_n, u32 towers) {
+    const u64 step = (u64)gridDim.x * blockDim.x;
+    const u64 poly = (u64)towers << log_n;
+    for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < npairs; i += step) {
+        const PairIndex p = pair_index(i, log_n, towers);
+        const KsTower T = tw[p.t];
+        const u64 inner = ((u64)p.t << log_n) + p.c;
+        const u64* d = digits + (u64)p.b * beta * poly + inner;
+        const u64* pb = kb + T.key_off + p.c;
+        const u64* pa = ka + T.key_off + p.c;
+        u64 b0l = 0, b0h = 0, b1l = 0, b1h = 0, a0l = 0, a0h = 0, a1l = 0, a1h = 0;
+        for (u32 j = 0; j < beta; j++) {
+            const ulonglong2 x = *reinterpret_cast<const ulonglong2*>(d + (u64)j * poly);
+            const ulonglong2 vb = *reinterpret_cast<const ulonglong2*>(pb + (u64)j * key_stride);
+            const ulonglong2 va = *reinterpret_cast<const ulonglong2*>(pa + (u64)j * key_stride);
+            u64 l, h;
+            mul128(x.x, vb.x, l, h);
+            b0l += l;
+            b0h += h + (b0l < l);
+            mul128(x.y, vb.y, l, h);
+            b1l += l;
+            b1h += h + (b1l < l);
+            mul128(x.x, va.x, l, h);
+            a0l += l;
+            a0h += h + (a0l < l);
+            mul128(x.y, va.y, l, h);
+            a1l += l;
+            a1h += h + (a1l < l);
+        }
+        const u64 o = (u64)p.b * poly + inner;
+        *reinterpret_cast<ulonglong2*>(ct0 + o) = make_ulonglong2(barrett128(b0l, b0h, T.m, T.mu_lo, T.mu_hi),
+                                                                  barrett128(b1l, b1h, T.m, T.mu_lo, T.mu_hi));
+        *reinterpret_cast<ulonglong2*>(ct1 + o) = make_ulonglong2(barrett128(a0l, a0h, T.m, T.mu_lo, T.mu_hi),
+                                                                  barrett128(a1l, a1h, T.m, T.mu_lo, T.mu_hi));
+    }
+}
+
+// NativeVectorT::SwitchModulus (mubintvecnat.cpp:111-136), value for value.
+__global__ __launch_bounds__(256) void k_switch_modulus(const u64* src, u64* dst, u64 n, u64 om, u64 nm) {
+    const u64 step = (u64)gridDim.x * blockDim.x;
+    const u64 half = om >> 1;
+    const bool up = nm > om;
+    const u64 diff = up ? nm - om : nm - (om % nm);
+    for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += step) {
+        u64 v = src[i];
+        if (v > half) v += diff;
+        if (!up && v >= nm) v %= nm;
+        dst[i] = v;
+    }
+}
+
+// PolyImpl::AutomorphismTransform(k) (poly-impl.h:338-364).  One thread per
+// index j of one (batch, tower) row:
+//   evaluation form:  dst[rev(j)] = src[rev(((k (2j+1)) >> 1) mod n)]
+//   coefficient form: dst[(j k) mod n] = bit_logn(j k) ? q - src[j] : src[j]
+// (products taken mod 2n, which is what the reference's wrapping uint32
+// arithmetic keeps, 2n dividing 2^32).
+template <bool EVAL>
+__global__ __launch_bounds__(256) void k_automorphism(const TowerConst* __restrict__ tcs, const u64* src, u64* dst,
+                                                      u32 k, u64 total, u32 log_n, u32 towers) {
+    const u64 step = (u64)gridDim.x * blockDim.x;
+    const u64 n = 1ull << log_n, mask = n - 1, m2 = 2 * n - 1;
+    for (u64 e = (u64)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += step) {
+        const u64 row = e >> log_n;
+        const u64 j = e & mask;
+        const u64 base = row << log_n;
+        if (EVAL) {
+            const u64 jk = ((u64)k * (2 * j + 1)) & m2;
+            const u32 jrev = __builtin_bitreverse32((u32)j) >> (32 - log_n);
+            const u32 irev = __builtin_bitreverse32((u32)((jk >> 1) & mask)) >> (32 - log_n);
+            dst[base + jrev] = src[base + irev];
+        } else {
+            const u64 q = tcs[row % towers].q;
+            const u64 jk = ((u64)k * j) & m2;
+            const u64 v = src[base + j];
+            dst[base + (jk & mask)] = ((jk >> log_n) & 1) ? q - v : v;
+        }
+    }
+}
+
+}  // namespace ofhe

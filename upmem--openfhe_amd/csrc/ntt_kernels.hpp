@@ -51,8 +51,10 @@ struct PlanArgs {
     const u64* tw;         // [T][N][2]   forward Table (bit-reversed powers of psi)
     const u64* itw;        // [T][N][2]   inverse TableI
     const u64* itwn;       // [T][N/2][2] TableI[N/2 + i] * N^-1 (first inverse stage)
+    u64 sstride;           // words between batch entries of src (towers * N when dense)
+    u64 dstride;           // words between batch entries of dst (and of the Hadamard operand)
     u32 log_n;
-    u32 towers;
+    u32 towers;            // towers in this launch (a plan range starts at tc[0])
 };
 
 enum { MODE_FWD = 0, MODE_INV = 1, MODE_FUSED = 2 };
@@ -195,8 +197,9 @@ __global__ __launch_bounds__(256, OFHE_KB_WAVES) void k_block(PlanArgs P, const 
     const u32 g = wid % G;
     const u32 pb = wid / G;
     const u32 t = pb / batch, b = pb % batch;
-    const u64 off = ((u64)b * P.towers + t) * N + ((u64)g << 12);
-    const u64* blk = src + off;
+    const u64 inner = (u64)t * N + ((u64)g << 12);
+    const u64 off = (u64)b * P.dstride + inner;
+    const u64* blk = src + (u64)b * P.sstride + inner;
     u64* oblk = dst + off;
     const TowerConst tc = P.tc[t];
     const u64 q = tc.q;
@@ -315,9 +318,9 @@ __global__ __launch_bounds__(256, OFHE_KB_WAVES) void k_tcols(PlanArgs P, const 
     const u32 cb = wid % (S / 16);
     const u32 pb = wid / (S / 16);
     const u32 t = pb / batch, b = pb % batch;
-    const u64 off = ((u64)b * P.towers + t) * N + cb * 16;
-    const u64* x = src + off;
-    u64* y = dst + off;
+    const u64 inner = (u64)t * N + cb * 16;
+    const u64* x = src + (u64)b * P.sstride + inner;
+    u64* y = dst + (u64)b * P.dstride + inner;
     const TowerConst tc = P.tc[t];
     const u64 q = tc.q;
     const Mod<SPQ> M = load_mod<SPQ>(tc);
@@ -402,9 +405,9 @@ __global__ __launch_bounds__(256) void k_cols(PlanArgs P, const u64* src, u64* d
     const u32 cb = wid % CB;
     const u32 pb = wid / CB;
     const u32 t = pb / batch, b = pb % batch;
-    const u64 off = ((u64)b * P.towers + t) * N + cb * (256 * CPT) + threadIdx.x * CPT;
-    const u64* x = src + off;
-    u64* y = dst + off;
+    const u64 inner = (u64)t * N + cb * (256 * CPT) + threadIdx.x * CPT;
+    const u64* x = src + (u64)b * P.sstride + inner;
+    u64* y = dst + (u64)b * P.dstride + inner;
     const TowerConst tc = P.tc[t];
     const u64 q = tc.q;
     const Mod<SPQ> M = load_mod<SPQ>(tc);
@@ -446,8 +449,9 @@ __global__ __launch_bounds__(256) void k_small(PlanArgs P, const u64* src, u64* 
     __shared__ u64 lds[2048];
     const u32 logn = P.log_n, N = 1u << logn, half = N >> 1;
     const u32 pb = blockIdx.x;
-    const u32 t = pb % P.towers;
-    const u64 off = (u64)pb * N;
+    const u32 t = pb % P.towers, b = pb / P.towers;
+    const u64 soff = (u64)b * P.sstride + (u64)t * N;
+    const u64 off = (u64)b * P.dstride + (u64)t * N;
     const TowerConst tc = P.tc[t];
     const u64 q = tc.q;
     const Mod<SPQ> M = load_mod<SPQ>(tc);
@@ -455,7 +459,7 @@ __global__ __launch_bounds__(256) void k_small(PlanArgs P, const u64* src, u64* 
     const u64* itw = P.itw + (u64)t * N * 2;
     const u64* itwn = P.itwn + (u64)t * N;
     (void)batch;
-    for (u32 i = threadIdx.x; i < N; i += blockDim.x) lds[i] = src[off + i];
+    for (u32 i = threadIdx.x; i < N; i += blockDim.x) lds[i] = src[soff + i];
     __syncthreads();
     if (MODE == MODE_FWD || MODE == MODE_FUSED) {
         for (u32 m = 1, lt = logn - 1; m < N; m <<= 1, lt--) {

@@ -10,99 +10,30 @@
 //   ChineseRemainderTransformFTTNat static tables (transformnat-impl.h:708-763)
 //     -> ofhe_plan_s, device-resident twiddles per (q, N).
 // No CPU fallback: every compute entry point launches HIP kernels or fails.
-#include <hip/hip_runtime.h>
-
-#include <atomic>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
-#include <mutex>
 #include <new>
-#include <string>
 #include <thread>
-#include <vector>
 
-#include "../../include/ofhe_hip.h"
-#include "eltwise_kernels.hpp"
+#include "internal.hpp"
 
 using namespace ofhe;
-typedef unsigned __int128 u128;
 
-#define OFHE_VERSION "ofhe-hip 0.1 gfx950"
+#define OFHE_VERSION "ofhe-hip 0.2 gfx950"
 
-namespace {
-
-thread_local std::string g_err;
-
+namespace ofhe {
+static thread_local std::string g_err;
 int fail(int code, const std::string& msg) {
     g_err = msg;
     return code;
 }
-
-#define HIPCHK(call)                                                                        \
-    do {                                                                                    \
-        hipError_t e_ = (call);                                                             \
-        if (e_ != hipSuccess)                                                               \
-            return fail(OFHE_ERR_HIP, std::string(#call) + ": " + hipGetErrorString(e_));  \
-    } while (0)
-
-// ---- host-side number theory for table construction (setup, not timed) ----
-u64 mulmod(u64 a, u64 b, u64 q) { return (u64)(((u128)a * b) % q); }
-u64 powmod(u64 b, u64 e, u64 q) {
-    u64 r = 1 % q;
-    b %= q;
-    while (e) {
-        if (e & 1) r = mulmod(r, b, q);
-        b = mulmod(b, b, q);
-        e >>= 1;
-    }
-    return r;
+int post_launch() {
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return fail(OFHE_ERR_HIP, std::string("kernel launch: ") + hipGetErrorString(e));
+    return OFHE_OK;
 }
-u64 invmod(u64 a, u64 q) { return powmod(a, q - 2, q); }  // q prime
-u64 shoup_pre(u64 w, u64 q) { return (u64)(((u128)w << 64) / q); }
-unsigned msb64(u64 x) { return x ? 64u - (unsigned)__builtin_clzll(x) : 0u; }
-u32 bitrev(u32 x, unsigned bits) {
-    u32 r = 0;
-    for (unsigned i = 0; i < bits; i++) {
-        r = (r << 1) | (x & 1);
-        x >>= 1;
-    }
-    return r;
-}
-
-}  // namespace
-
-struct ofhe_ctx_s {
-    int device = 0;
-    std::atomic<int> live{1};
-};
-
-struct ofhe_plan_s {
-    ofhe_ctx_t ctx = nullptr;
-    u32 log_n = 0, towers = 0;
-    // device
-    TowerConst* d_tc = nullptr;
-    u64* d_tw = nullptr;
-    u64* d_itw = nullptr;
-    u64* d_itwn = nullptr;
-    // host copies (for ofhe_hip_plan_tables and scalar prep)
-    std::vector<u64> q, tab, tab_pre, itab, itab_pre, ninv;
-    u64* d_scal = nullptr;  // scratch for per-tower scalars (modmul_scalar)
-    std::mutex scal_mu;
-    // pipeline tuning (ofhe_hip_plan_tune): batch entries per chunk (0 = all)
-    // and internal streams the chunks alternate over (1 = caller's stream).
-    u32 chunk_batch = 0, nstreams = 1;
-    bool spq = false;     // every modulus is 2^L - d with d < 2^32 (special-prime kernels)
-    bool split8 = false;  // log_n == 16: 8 column stages + 8 block stages (k_tcols + k_block<.,.,2>)
-    hipStream_t st[2] = {nullptr, nullptr};
-    hipEvent_t ev_fork = nullptr, ev_join[2] = {nullptr, nullptr};
-};
-
-struct ofhe_bconv_s {
-    ofhe_ctx_t ctx = nullptr;
-    BconvArgs args{};
-    u64* d_mem = nullptr;
-};
+}  // namespace ofhe
 
 // Entry points keep the C linkage of their declarations in include/ofhe_hip.h.
 const char* ofhe_hip_last_error(void) { return g_err.c_str(); }
@@ -151,31 +82,51 @@ int ofhe_hip_free(ofhe_ctx_t ctx, void* dptr) {
     return OFHE_OK;
 }
 
-// NULL selects the device's default (null) stream, as the header documents;
-// callers that want overlap pass their own stream (e.g. torch's).
-static hipStream_t pick(ofhe_ctx_t, void* stream) { return (hipStream_t)stream; }
+
+int ofhe_hip_alloc_async(ofhe_ctx_t ctx, size_t bytes, void** dptr, void* stream) {
+    if (!ctx || !dptr) return fail(OFHE_ERR_ARG, "NULL argument");
+    HIPCHK(hipSetDevice(ctx->device));
+    hipError_t e = hipMallocAsync(dptr, bytes ? bytes : 1, pick(stream));
+    if (e != hipSuccess) return fail(OFHE_ERR_NOMEM, std::string("hipMallocAsync: ") + hipGetErrorString(e));
+    return OFHE_OK;
+}
+
+int ofhe_hip_free_async(ofhe_ctx_t ctx, void* dptr, void* stream) {
+    if (!ctx) return fail(OFHE_ERR_ARG, "ctx is NULL");
+    if (!dptr) return OFHE_OK;
+    HIPCHK(hipSetDevice(ctx->device));
+    HIPCHK(hipFreeAsync(dptr, pick(stream)));
+    return OFHE_OK;
+}
+
+int ofhe_hip_zero(ofhe_ctx_t ctx, void* dst, size_t bytes, void* stream) {
+    if (!ctx || (!dst && bytes)) return fail(OFHE_ERR_ARG, "NULL argument");
+    if (!bytes) return OFHE_OK;
+    HIPCHK(hipMemsetAsync(dst, 0, bytes, pick(stream)));
+    return OFHE_OK;
+}
 
 int ofhe_hip_copy_to_device(ofhe_ctx_t ctx, void* dst, const void* src, size_t bytes, void* stream) {
     if (!ctx || (!dst && bytes) || (!src && bytes)) return fail(OFHE_ERR_ARG, "NULL argument");
-    HIPCHK(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, pick(ctx, stream)));
+    HIPCHK(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, pick(stream)));
     return OFHE_OK;
 }
 
 int ofhe_hip_copy_to_host(ofhe_ctx_t ctx, void* dst, const void* src, size_t bytes, void* stream) {
     if (!ctx || (!dst && bytes) || (!src && bytes)) return fail(OFHE_ERR_ARG, "NULL argument");
-    HIPCHK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, pick(ctx, stream)));
+    HIPCHK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, pick(stream)));
     return OFHE_OK;
 }
 
 int ofhe_hip_copy_device(ofhe_ctx_t ctx, void* dst, const void* src, size_t bytes, void* stream) {
     if (!ctx || (!dst && bytes) || (!src && bytes)) return fail(OFHE_ERR_ARG, "NULL argument");
-    HIPCHK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, pick(ctx, stream)));
+    HIPCHK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, pick(stream)));
     return OFHE_OK;
 }
 
 int ofhe_hip_sync(ofhe_ctx_t ctx, void* stream) {
     if (!ctx) return fail(OFHE_ERR_ARG, "ctx is NULL");
-    HIPCHK(hipStreamSynchronize(pick(ctx, stream)));
+    HIPCHK(hipStreamSynchronize(pick(stream)));
     return OFHE_OK;
 }
 
@@ -204,6 +155,7 @@ int ofhe_hip_plan_create(ofhe_ctx_t ctx, uint32_t log_n, uint32_t towers, const 
     p->towers = towers;
     const size_t TN = (size_t)towers * N;
     p->q.assign(q, q + towers);
+    p->psi.assign(psi, psi + towers);
     p->tab.resize(TN);
     p->tab_pre.resize(TN);
     p->itab.resize(TN);
@@ -336,14 +288,19 @@ int ofhe_hip_plan_tables(ofhe_plan_t p, uint64_t* tab, uint64_t* tab_pre, uint64
 // ---------------------------------------------------------------------------
 // Launch helpers
 // ---------------------------------------------------------------------------
-static PlanArgs args_of(ofhe_plan_t p) {
+// Device view of plan towers [t0, t0 + count); dense [batch][count][N] strides
+// unless the caller overrides them.
+static PlanArgs args_of(ofhe_plan_t p, u32 t0 = 0, u32 count = 0) {
+    if (!count) count = p->towers - t0;
+    const u64 N = 1ull << p->log_n;
     PlanArgs a;
-    a.tc = p->d_tc;
-    a.tw = p->d_tw;
-    a.itw = p->d_itw;
-    a.itwn = p->d_itwn;
+    a.tc = p->d_tc + t0;
+    a.tw = p->d_tw + 2 * N * t0;
+    a.itw = p->d_itw + 2 * N * t0;
+    a.itwn = p->d_itwn + N * t0;
+    a.sstride = a.dstride = N * count;
     a.log_n = p->log_n;
-    a.towers = p->towers;
+    a.towers = count;
     return a;
 }
 
@@ -440,42 +397,70 @@ static void launch_colpass(const PlanArgs& a, bool spq, bool split8, bool inv, c
         launch_cols(a, spq, inv, src, dst, batch, s);
 }
 
-static int post_launch() {
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return fail(OFHE_ERR_HIP, std::string("kernel launch: ") + hipGetErrorString(e));
-    return OFHE_OK;
-}
 
-int ofhe_hip_ntt_fwd(ofhe_plan_t p, uint64_t* data, uint32_t batch, void* stream) {
-    int rc = check_common(p, batch);
-    if (rc) return rc;
-    if (!data) return fail(OFHE_ERR_ARG, "data is NULL");
+namespace ofhe {
+int plan_ntt_range(ofhe_plan_t p, bool inverse, u32 t0, u32 count, const u64* src, u64* dst, u64 sstride,
+                   u64 dstride, u32 batch, hipStream_t s) {
+    if (!p || !p->ctx) return fail(OFHE_ERR_STATE, "plan is NULL or destroyed");
+    if (count == 0 || batch == 0) return OFHE_OK;
+    if (t0 + count > p->towers || t0 + count < t0) return fail(OFHE_ERR_ARG, "tower range outside the plan");
+    if (!src || !dst) return fail(OFHE_ERR_ARG, "data is NULL");
+    const u64 N = 1ull << p->log_n;
+    if (sstride < N * count || dstride < N * count)
+        return fail(OFHE_ERR_ARG, "batch stride smaller than the tower range");
+    if ((u64)batch * count * N / 4096 >= (1ull << 31)) return fail(OFHE_ERR_ARG, "batch too large for one launch");
     HIPCHK(hipSetDevice(p->ctx->device));
-    const PlanArgs a = args_of(p);
-    hipStream_t s = pick(p->ctx, stream);
-    if (p->log_n < 12) {
-        launch_small<MODE_FWD>(a, p->spq, data, data, nullptr, batch, s);
+    PlanArgs a = args_of(p, t0, count);
+    PlanArgs ad = a;  // second pass: dst -> dst
+    a.sstride = sstride;
+    a.dstride = ad.sstride = ad.dstride = dstride;
+    if (!inverse) {
+        if (p->log_n < 12) {
+            launch_small<MODE_FWD>(a, p->spq, src, dst, nullptr, batch, s);
+        } else if (p->log_n == 12) {
+            launch_block<MODE_FWD>(a, p->spq, src, dst, nullptr, batch, s, p->split8);
+        } else {
+            launch_colpass(a, p->spq, p->split8, false, src, dst, batch, s);
+            launch_block<MODE_FWD>(ad, p->spq, dst, dst, nullptr, batch, s, p->split8);
+        }
     } else {
-        if (p->log_n > 12) launch_colpass(a, p->spq, p->split8, false, data, data, batch, s);
-        launch_block<MODE_FWD>(a, p->spq, data, data, nullptr, batch, s, p->split8);
+        if (p->log_n < 12) {
+            launch_small<MODE_INV>(a, p->spq, src, dst, nullptr, batch, s);
+        } else {
+            launch_block<MODE_INV>(a, p->spq, src, dst, nullptr, batch, s, p->split8);
+            if (p->log_n > 12) launch_colpass(ad, p->spq, p->split8, true, dst, dst, batch, s);
+        }
     }
     return post_launch();
+}
+}  // namespace ofhe
+
+int ofhe_hip_ntt_fwd(ofhe_plan_t p, uint64_t* data, uint32_t batch, void* stream) {
+    RCCHK(check_common(p, batch));
+    if (!data) return fail(OFHE_ERR_ARG, "data is NULL");
+    const u64 d = (u64)p->towers << p->log_n;
+    return plan_ntt_range(p, false, 0, p->towers, data, data, d, d, batch, pick(stream));
 }
 
 int ofhe_hip_ntt_inv(ofhe_plan_t p, uint64_t* data, uint32_t batch, void* stream) {
-    int rc = check_common(p, batch);
-    if (rc) return rc;
+    RCCHK(check_common(p, batch));
     if (!data) return fail(OFHE_ERR_ARG, "data is NULL");
-    HIPCHK(hipSetDevice(p->ctx->device));
-    const PlanArgs a = args_of(p);
-    hipStream_t s = pick(p->ctx, stream);
-    if (p->log_n < 12) {
-        launch_small<MODE_INV>(a, p->spq, data, data, nullptr, batch, s);
-    } else {
-        launch_block<MODE_INV>(a, p->spq, data, data, nullptr, batch, s, p->split8);
-        if (p->log_n > 12) launch_colpass(a, p->spq, p->split8, true, data, data, batch, s);
-    }
-    return post_launch();
+    const u64 d = (u64)p->towers << p->log_n;
+    return plan_ntt_range(p, true, 0, p->towers, data, data, d, d, batch, pick(stream));
+}
+
+int ofhe_hip_ntt_fwd_range(ofhe_plan_t p, uint32_t t0, uint32_t count, const uint64_t* src, uint64_t* dst,
+                           uint64_t src_stride, uint64_t dst_stride, uint32_t batch, void* stream) {
+    if (!p || !p->ctx) return fail(OFHE_ERR_STATE, "plan is NULL or destroyed");
+    if (batch == 0 || count == 0) return fail(OFHE_ERR_ARG, "batch and count must be >= 1");
+    return plan_ntt_range(p, false, t0, count, src, dst, src_stride, dst_stride, batch, pick(stream));
+}
+
+int ofhe_hip_ntt_inv_range(ofhe_plan_t p, uint32_t t0, uint32_t count, const uint64_t* src, uint64_t* dst,
+                           uint64_t src_stride, uint64_t dst_stride, uint32_t batch, void* stream) {
+    if (!p || !p->ctx) return fail(OFHE_ERR_STATE, "plan is NULL or destroyed");
+    if (batch == 0 || count == 0) return fail(OFHE_ERR_ARG, "batch and count must be >= 1");
+    return plan_ntt_range(p, true, t0, count, src, dst, src_stride, dst_stride, batch, pick(stream));
 }
 
 int ofhe_hip_ntt_mul_intt(ofhe_plan_t p, const uint64_t* a_, const uint64_t* b, uint64_t* c,
@@ -486,7 +471,7 @@ int ofhe_hip_ntt_mul_intt(ofhe_plan_t p, const uint64_t* a_, const uint64_t* b, 
     if (b == c && a_ != c) return fail(OFHE_ERR_ARG, "c may alias a but not b");
     HIPCHK(hipSetDevice(p->ctx->device));
     const PlanArgs a = args_of(p);
-    hipStream_t s = pick(p->ctx, stream);
+    hipStream_t s = pick(stream);
     if (p->log_n < 12) {
         launch_small<MODE_FUSED>(a, p->spq, a_, c, b, batch, s);
     } else if (p->log_n == 12) {
@@ -530,7 +515,7 @@ int ofhe_hip_ntt_mul_intt_stage(ofhe_plan_t p, int stage, const uint64_t* a_, co
     if (stage < 0 || stage > 2) return fail(OFHE_ERR_ARG, "stage must be 0, 1 or 2");
     HIPCHK(hipSetDevice(p->ctx->device));
     const PlanArgs a = args_of(p);
-    hipStream_t s = pick(p->ctx, stream);
+    hipStream_t s = pick(stream);
     if (p->log_n < 12) {
         if (stage == 1) launch_small<MODE_FUSED>(a, p->spq, a_, c, b, batch, s);
     } else if (p->log_n == 12) {
@@ -554,7 +539,7 @@ static int eltwise(ofhe_plan_t p, const u64* a, const u64* b, u64* c, u32 batch,
     const u64 npairs = (u64)batch * p->towers * ((u64)1 << p->log_n) / 2;
     u64 blocks = (npairs + 255) / 256;
     if (blocks > 256 * 16) blocks = 256 * 16;
-    hipLaunchKernelGGL((k_eltwise<OP>), dim3((u32)blocks), dim3(256), 0, pick(p->ctx, stream), p->d_tc, a, b,
+    hipLaunchKernelGGL((k_eltwise<OP>), dim3((u32)blocks), dim3(256), 0, pick(stream), p->d_tc, a, b,
                        c, npairs, p->log_n, p->towers);
     return post_launch();
 }
@@ -589,7 +574,7 @@ int ofhe_hip_modmul_scalar(ofhe_plan_t p, const uint64_t* a, const uint64_t* s, 
     // the plan's mutex so concurrent callers on one plan do not race on it.
     std::lock_guard<std::mutex> lk(p->scal_mu);
     HIPCHK(hipSetDevice(p->ctx->device));
-    hipStream_t st = pick(p->ctx, stream);
+    hipStream_t st = pick(stream);
     HIPCHK(hipMemcpyAsync(p->d_scal, sp.data(), sizeof(u64) * sp.size(), hipMemcpyHostToDevice, st));
     HIPCHK(hipStreamSynchronize(st));
     return eltwise<ELT_MULS>(p, a, p->d_scal, c, batch, stream);
@@ -649,6 +634,10 @@ int ofhe_hip_bconv_create(ofhe_ctx_t ctx, uint32_t log_n, uint32_t size_q, uint3
     A.log_n = log_n;
     A.size_q = size_q;
     A.size_p = size_p;
+    A.in_stride = (u64)size_q << log_n;
+    A.out_stride = (u64)size_p << log_n;
+    A.gap_at = size_p;
+    A.gap = 0;
     *out = b;
     return OFHE_OK;
 }
@@ -661,16 +650,20 @@ int ofhe_hip_bconv_destroy(ofhe_bconv_t b) {
     return OFHE_OK;
 }
 
+namespace ofhe {
+int bconv_run(const BconvArgs& A, const u64* x, u64* out, u32 batch, hipStream_t s) {
+    const u64 total = (u64)batch << A.log_n;
+    const u64 blocks = (total + 255) / 256;
+    if (blocks >= (1ull << 31)) return fail(OFHE_ERR_ARG, "batch too large");
+    hipLaunchKernelGGL((k_bconv<8>), dim3((u32)blocks), dim3(256), 0, s, A, x, out, batch);
+    return post_launch();
+}
+}  // namespace ofhe
+
 int ofhe_hip_approx_switch_crt_basis(ofhe_bconv_t b, const uint64_t* x, uint64_t* out, uint32_t batch,
                                      void* stream) {
     if (!b || !b->ctx) return fail(OFHE_ERR_STATE, "bconv is NULL or destroyed");
     if (!x || !out || batch == 0) return fail(OFHE_ERR_ARG, "bad data argument");
     HIPCHK(hipSetDevice(b->ctx->device));
-    const u64 total = (u64)batch << b->args.log_n;
-    const u64 blocks = (total + 255) / 256;
-    if (blocks >= (1ull << 31)) return fail(OFHE_ERR_ARG, "batch too large");
-    hipLaunchKernelGGL((k_bconv<8>), dim3((u32)blocks), dim3(256), 0, pick(b->ctx, stream), b->args, x, out,
-                       batch);
-    return post_launch();
+    return bconv_run(b->args, x, out, batch, pick(stream));
 }
-

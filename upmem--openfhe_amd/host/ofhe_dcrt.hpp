@@ -59,16 +59,26 @@ public:
     }
     ofhe_ctx_t ctx() const { return ctx_; }
     int device() const { return device_; }
+    // Stream-ordered on the default stream every adapter op uses: a buffer
+    // dropped while kernels that read it are still queued stays valid until
+    // they finish (DCRTPoly temporaries die right after the call that uses them).
     void* allocate(size_t bytes) {
         void* p = nullptr;
-        check(ofhe_hip_alloc(ctx_, bytes, &p), "HipManager::allocate");
+        check(ofhe_hip_alloc_async(ctx_, bytes, &p, nullptr), "HipManager::allocate");
         return p;
     }
-    void deallocate(void* p) { check(ofhe_hip_free(ctx_, p), "HipManager::deallocate"); }
+    void deallocate(void* p) { check(ofhe_hip_free_async(ctx_, p, nullptr), "HipManager::deallocate"); }
+    void zero(void* dst, size_t bytes) { check(ofhe_hip_zero(ctx_, dst, bytes, nullptr), "HipManager::zero"); }
+    // Host <-> device copies of pageable memory are bracketed by stream syncs:
+    // HIP may stage them outside the stream's order, and the host buffer may
+    // be released as soon as the call returns.
     void copy_to_device(void* dst, const void* src, size_t bytes) {
+        sync();
         check(ofhe_hip_copy_to_device(ctx_, dst, src, bytes, nullptr), "HipManager::copy_to_device");
+        sync();
     }
     void copy_from_device(void* dst, const void* src, size_t bytes) {
+        sync();
         check(ofhe_hip_copy_to_host(ctx_, dst, src, bytes, nullptr), "HipManager::copy_from_device");
         sync();
     }
@@ -100,11 +110,12 @@ public:
         return *this;
     }
     ~DeviceBuffer() {
-        if (p_) ofhe_hip_free(m_->ctx(), p_);
+        if (p_) ofhe_hip_free_async(m_->ctx(), p_, nullptr);
     }
     uint64_t* get() const { return p_; }
     size_t size() const { return n_; }
     void upload(const uint64_t* h) { m_->copy_to_device(p_, h, n_ * 8); }
+    void zero() { m_->zero(p_, n_ * 8); }
     void download(uint64_t* h) const { m_->copy_from_device(h, p_, n_ * 8); }
     void copy_from(const DeviceBuffer& o) {
         check(ofhe_hip_copy_device(m_->ctx(), p_, o.p_, n_ * 8, nullptr), "DeviceBuffer::copy_from");
@@ -172,8 +183,7 @@ public:
     DCRTPolyHip(std::shared_ptr<DCRTParams> p, Format f, uint32_t batch = 1)
         : p_(std::move(p)), f_(f), batch_(batch),
           buf_(p_->manager(), (size_t)batch * p_->Towers() * p_->GetRingDimension()) {
-        std::vector<uint64_t> z(buf_.size(), 0);
-        buf_.upload(z.data());
+        buf_.zero();
     }
     DCRTPolyHip(const DCRTPolyHip& o) : p_(o.p_), f_(o.f_), batch_(o.batch_), buf_(o.p_->manager(), o.buf_.size()) {
         buf_.copy_from(o.buf_);
@@ -276,6 +286,14 @@ public:
         return r;
     }
 
+    // AutomorphismTransform(k) (dcrtpoly-impl.h:350-358 -> poly-impl.h:312-365)
+    DCRTPolyHip AutomorphismTransform(uint32_t k) const {
+        DCRTPolyHip r(p_, f_, batch_);
+        check(ofhe_hip_automorphism(p_->plan(), k, f_ == Format::EVALUATION, data(), r.data(), batch_, nullptr),
+              "AutomorphismTransform");
+        return r;
+    }
+
     bool operator==(const DCRTPolyHip& o) const {
         return f_ == o.f_ && p_->Moduli() == o.p_->Moduli() && GetValues() == o.GetValues();
     }
@@ -322,8 +340,82 @@ public:
         return out;
     }
 
+    ofhe_bconv_t handle() const { return h_; }
+
 private:
     ofhe_bconv_t h_ = nullptr;
+};
+
+// ApproxModUp (dcrtpoly-impl.h:1085-1131): x over Q (either format) -> a
+// polynomial over paramsQP = Q|P in EVALUATION form.  q_to_p converts Q -> P.
+inline DCRTPolyHip ApproxModUp(const DCRTPolyHip& x, const std::shared_ptr<DCRTParams>& paramsP,
+                               const std::shared_ptr<DCRTParams>& paramsQP, const BaseConverter& q_to_p) {
+    const auto& Q = x.GetParams();
+    if (paramsQP->Towers() != Q->Towers() + paramsP->Towers()) throw math_error("ApproxModUp: paramsQP size");
+    DCRTPolyHip out(paramsQP, Format::EVALUATION, x.Batch());
+    check(ofhe_hip_approx_mod_up(Q->plan(), paramsP->plan(), q_to_p.handle(), x.GetFormat() == Format::EVALUATION,
+                                 x.data(), out.data(), x.Batch(), nullptr),
+          "ApproxModUp");
+    return out;
+}
+
+// ApproxModDown (dcrtpoly-impl.h:1134-1175): x over Q|P (EVALUATION) -> Q.
+inline DCRTPolyHip ApproxModDown(const DCRTPolyHip& x, const std::shared_ptr<DCRTParams>& paramsQ,
+                                 const std::shared_ptr<DCRTParams>& paramsP, const BaseConverter& p_to_q,
+                                 const std::vector<uint64_t>& PInvModq, uint64_t t = 0) {
+    if (x.GetFormat() != Format::EVALUATION) throw math_error("ApproxModDown: EVALUATION form expected");
+    if (x.GetParams()->Towers() != paramsQ->Towers() + paramsP->Towers())
+        throw math_error("ApproxModDown: tower count mismatch");
+    if (PInvModq.size() != paramsQ->Towers()) throw math_error("ApproxModDown: PInvModq size");
+    DCRTPolyHip out(paramsQ, Format::EVALUATION, x.Batch());
+    check(ofhe_hip_approx_mod_down(paramsQ->plan(), paramsP->plan(), p_to_q.handle(), PInvModq.data(), t, x.data(),
+                                   out.data(), x.Batch(), nullptr),
+          "ApproxModDown");
+    return out;
+}
+
+// KeySwitchHYBRID (pke/lib/keyswitch/keyswitch-hybrid.cpp) for one parameter
+// set: Q (element params), P (GetParamsP()) and dnum = numPartQ.  An
+// evaluation key is a pair of DCRTPolyHip over Q|P with batch = numPartQ
+// (the b and a vectors of EvalKeyRelin).
+class KeySwitchHybrid {
+public:
+    KeySwitchHybrid(const DCRTParams& Q, const DCRTParams& P, uint32_t numPartQ) {
+        check(ofhe_hip_ks_create(Q.manager()->ctx(), Q.LogN(), (uint32_t)Q.Towers(), Q.Moduli().data(),
+                                 Q.Roots().data(), (uint32_t)P.Towers(), P.Moduli().data(), P.Roots().data(), numPartQ,
+                                 &h_),
+              "KeySwitchHybrid");
+        sizeQ_ = Q.Towers();
+        sizeP_ = P.Towers();
+        numPartQ_ = numPartQ;
+    }
+    ~KeySwitchHybrid() {
+        if (h_) ofhe_hip_ks_destroy(h_);
+    }
+    KeySwitchHybrid(const KeySwitchHybrid&) = delete;
+    KeySwitchHybrid& operator=(const KeySwitchHybrid&) = delete;
+
+    // KeySwitchCore(a, evalKey) (keyswitch-hybrid.cpp:325-328): c is over Ql
+    // (its params give the level), EVALUATION form.  t > 0 for BGV.
+    std::pair<DCRTPolyHip, DCRTPolyHip> KeySwitchCore(const DCRTPolyHip& c, const DCRTPolyHip& key_b,
+                                                      const DCRTPolyHip& key_a, uint64_t t = 0) const {
+        if (c.GetFormat() != Format::EVALUATION) throw math_error("KeySwitchCore: EVALUATION form expected");
+        const uint32_t l = (uint32_t)c.GetParams()->Towers();
+        if (l > sizeQ_) throw math_error("KeySwitchCore: ciphertext has more towers than Q");
+        if (key_b.Batch() != numPartQ_ || key_a.Batch() != numPartQ_ ||
+            key_b.GetParams()->Towers() != sizeQ_ + sizeP_ || key_a.GetParams()->Towers() != sizeQ_ + sizeP_)
+            throw math_error("KeySwitchCore: evaluation key must be numPartQ polynomials over Q|P");
+        DCRTPolyHip o0(c.GetParams(), Format::EVALUATION, c.Batch()), o1(c.GetParams(), Format::EVALUATION, c.Batch());
+        check(ofhe_hip_ks_core(h_, l, c.data(), key_b.data(), key_a.data(), o0.data(), o1.data(), t, c.Batch(),
+                               nullptr),
+              "KeySwitchCore");
+        return {std::move(o0), std::move(o1)};
+    }
+
+private:
+    ofhe_ks_t h_ = nullptr;
+    size_t sizeQ_ = 0, sizeP_ = 0;
+    uint32_t numPartQ_ = 0;
 };
 
 }  // namespace ofhe

@@ -9,6 +9,12 @@ Host-side mirror of the reference's offload interface for the hot path:
   ``NativeVectorT`` element-wise ops (mubintvecnat.cpp:245-367) over
   [batch][tower][N] device buffers.
 * ``BaseConverter`` ~ ``DCRTPolyImpl::ApproxSwitchCRTBasis`` (dcrtpoly-impl.h:1034-1063).
+* ``approx_mod_up`` / ``approx_mod_down`` ~ ``DCRTPolyImpl::ApproxModUp`` /
+  ``ApproxModDown`` (dcrtpoly-impl.h:1085-1175).
+* ``KeySwitch`` ~ ``KeySwitchHYBRID`` (pke/lib/keyswitch/keyswitch-hybrid.cpp:325-482)
+  with the tables of ``CryptoParametersRNS::PrecomputeCRTTables``.
+* ``switch_modulus`` / ``NTTPlan.automorphism`` ~ ``NativeVectorT::SwitchModulus``
+  (mubintvecnat.cpp:111-136) / ``PolyImpl::AutomorphismTransform`` (poly-impl.h:312-365).
 
 Errors raise ``MathError`` (the analogue of ``lbcrypto::math_error`` thrown by
 ``OPENFHE_THROW``).  Pointers are plain integers (e.g. ``torch.Tensor.data_ptr()``)
@@ -45,6 +51,9 @@ _SIGS = {
     "ofhe_hip_finalize": (ctypes.c_int, [_vp]),
     "ofhe_hip_alloc": (ctypes.c_int, [_vp, ctypes.c_size_t, ctypes.POINTER(_vp)]),
     "ofhe_hip_free": (ctypes.c_int, [_vp, _vp]),
+    "ofhe_hip_alloc_async": (ctypes.c_int, [_vp, ctypes.c_size_t, ctypes.POINTER(_vp), _vp]),
+    "ofhe_hip_free_async": (ctypes.c_int, [_vp, _vp, _vp]),
+    "ofhe_hip_zero": (ctypes.c_int, [_vp, _vp, ctypes.c_size_t, _vp]),
     "ofhe_hip_copy_to_device": (ctypes.c_int, [_vp, _vp, _vp, ctypes.c_size_t, _vp]),
     "ofhe_hip_copy_to_host": (ctypes.c_int, [_vp, _vp, _vp, ctypes.c_size_t, _vp]),
     "ofhe_hip_copy_device": (ctypes.c_int, [_vp, _vp, _vp, ctypes.c_size_t, _vp]),
@@ -66,6 +75,28 @@ _SIGS = {
                                              _u64p, _u64p, _u64p, _u64p, ctypes.POINTER(_vp)]),
     "ofhe_hip_bconv_destroy": (ctypes.c_int, [_vp]),
     "ofhe_hip_approx_switch_crt_basis": (ctypes.c_int, [_vp, _vp, _vp, ctypes.c_uint32, _vp]),
+    "ofhe_hip_ntt_fwd_range": (ctypes.c_int, [_vp, ctypes.c_uint32, ctypes.c_uint32, _vp, _vp, ctypes.c_uint64,
+                                              ctypes.c_uint64, ctypes.c_uint32, _vp]),
+    "ofhe_hip_ntt_inv_range": (ctypes.c_int, [_vp, ctypes.c_uint32, ctypes.c_uint32, _vp, _vp, ctypes.c_uint64,
+                                              ctypes.c_uint64, ctypes.c_uint32, _vp]),
+    "ofhe_hip_approx_mod_up": (ctypes.c_int, [_vp, _vp, _vp, ctypes.c_int, _vp, _vp, ctypes.c_uint32, _vp]),
+    "ofhe_hip_approx_mod_down": (ctypes.c_int, [_vp, _vp, _vp, _u64p, ctypes.c_uint64, _vp, _vp,
+                                                ctypes.c_uint32, _vp]),
+    "ofhe_hip_ks_create": (ctypes.c_int, [_vp, ctypes.c_uint32, ctypes.c_uint32, _u64p, _u64p, ctypes.c_uint32,
+                                          _u64p, _u64p, ctypes.c_uint32, ctypes.POINTER(_vp)]),
+    "ofhe_hip_ks_destroy": (ctypes.c_int, [_vp]),
+    "ofhe_hip_ks_digits": (ctypes.c_int, [_vp, ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint32),
+                                          ctypes.POINTER(ctypes.c_uint32)]),
+    "ofhe_hip_ks_precompute": (ctypes.c_int, [_vp, ctypes.c_uint32, _vp, _vp, ctypes.c_uint32, _vp]),
+    "ofhe_hip_ks_fast_core_ext": (ctypes.c_int, [_vp, ctypes.c_uint32, _vp, _vp, _vp, _vp, _vp, ctypes.c_uint32,
+                                                 _vp]),
+    "ofhe_hip_ks_mod_down": (ctypes.c_int, [_vp, ctypes.c_uint32, _vp, _vp, ctypes.c_uint64, ctypes.c_uint32,
+                                            _vp]),
+    "ofhe_hip_ks_core": (ctypes.c_int, [_vp, ctypes.c_uint32, _vp, _vp, _vp, _vp, _vp, ctypes.c_uint64,
+                                        ctypes.c_uint32, _vp]),
+    "ofhe_hip_switch_modulus": (ctypes.c_int, [_vp, _vp, _vp, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64,
+                                               _vp]),
+    "ofhe_hip_automorphism": (ctypes.c_int, [_vp, ctypes.c_uint32, ctypes.c_int, _vp, _vp, ctypes.c_uint32, _vp]),
 }
 
 EXPORTED_SYMBOLS = tuple(_SIGS)
@@ -141,6 +172,17 @@ class Context:
 
     def free(self, ptr: int) -> None:
         _check(lib().ofhe_hip_free(self.handle, _vp(ptr)))
+
+    def alloc_async(self, nbytes: int, stream: int = 0) -> int:
+        p = _vp()
+        _check(lib().ofhe_hip_alloc_async(self.handle, int(nbytes), ctypes.byref(p), _vp(stream or None)))
+        return p.value
+
+    def free_async(self, ptr: int, stream: int = 0) -> None:
+        _check(lib().ofhe_hip_free_async(self.handle, _vp(ptr), _vp(stream or None)))
+
+    def zero(self, dst: int, nbytes: int, stream: int = 0) -> None:
+        _check(lib().ofhe_hip_zero(self.handle, _vp(dst), int(nbytes), _vp(stream or None)))
 
     def copy_to_device(self, dst: int, src: int, nbytes: int, stream: int = 0) -> None:
         _check(lib().ofhe_hip_copy_to_device(self.handle, _vp(dst), _vp(src), int(nbytes), _vp(stream or None)))
@@ -227,6 +269,22 @@ class NTTPlan:
         _check(lib().ofhe_hip_modmul_scalar(self.handle, _vp(a), _arr(scalars), _vp(c), int(batch),
                                             _vp(stream or None)))
 
+    # --- tower-range transforms on strided data ---
+    def forward_range(self, t0: int, count: int, src: int, dst: int, src_stride: int, dst_stride: int,
+                      batch: int = 1, stream: int = 0) -> None:
+        _check(lib().ofhe_hip_ntt_fwd_range(self.handle, int(t0), int(count), _vp(src), _vp(dst), int(src_stride),
+                                            int(dst_stride), int(batch), _vp(stream or None)))
+
+    def inverse_range(self, t0: int, count: int, src: int, dst: int, src_stride: int, dst_stride: int,
+                      batch: int = 1, stream: int = 0) -> None:
+        _check(lib().ofhe_hip_ntt_inv_range(self.handle, int(t0), int(count), _vp(src), _vp(dst), int(src_stride),
+                                            int(dst_stride), int(batch), _vp(stream or None)))
+
+    def automorphism(self, k: int, eval_form: bool, src: int, dst: int, batch: int = 1, stream: int = 0) -> None:
+        """PolyImpl::AutomorphismTransform(k) on every (batch, tower); dst must not alias src."""
+        _check(lib().ofhe_hip_automorphism(self.handle, int(k), 1 if eval_form else 0, _vp(src), _vp(dst),
+                                           int(batch), _vp(stream or None)))
+
     # --- the metric pipeline ---
     def ntt_mul_intt(self, a: int, b: int, c: int, batch: int = 1, stream: int = 0) -> None:
         _check(lib().ofhe_hip_ntt_mul_intt(self.handle, _vp(a), _vp(b), _vp(c), int(batch), _vp(stream or None)))
@@ -266,3 +324,77 @@ class BaseConverter:
 
     def switch(self, x: int, out: int, batch: int = 1, stream: int = 0) -> None:
         _check(lib().ofhe_hip_approx_switch_crt_basis(self._h, _vp(x), _vp(out), int(batch), _vp(stream or None)))
+
+
+def switch_modulus(ctx: Context, src: int, dst: int, n: int, old_q: int, new_q: int, stream: int = 0) -> None:
+    """NativeVectorT::SwitchModulus on n words of device memory."""
+    _check(lib().ofhe_hip_switch_modulus(ctx.handle, _vp(src), _vp(dst), int(n), int(old_q), int(new_q),
+                                         _vp(stream or None)))
+
+
+def approx_mod_up(plan_q: NTTPlan, plan_p: NTTPlan, q_to_p: BaseConverter, eval_form: bool, x: int, out: int,
+                  batch: int = 1, stream: int = 0) -> None:
+    """ApproxModUp: x [batch][Q][N] -> out [batch][Q+P][N] (evaluation form)."""
+    _check(lib().ofhe_hip_approx_mod_up(plan_q.handle, plan_p.handle, q_to_p._h, 1 if eval_form else 0, _vp(x),
+                                        _vp(out), int(batch), _vp(stream or None)))
+
+
+def approx_mod_down(plan_q: NTTPlan, plan_p: NTTPlan, p_to_q: BaseConverter, p_inv_modq: Sequence[int], t: int,
+                    x: int, out: int, batch: int = 1, stream: int = 0) -> None:
+    """ApproxModDown: x [batch][Q+P][N] -> out [batch][Q][N] (evaluation form)."""
+    if len(p_inv_modq) != plan_q.towers:
+        raise MathError("p_inv_modq needs one entry per Q tower")
+    _check(lib().ofhe_hip_approx_mod_down(plan_q.handle, plan_p.handle, p_to_q._h, _arr(p_inv_modq), int(t),
+                                          _vp(x), _vp(out), int(batch), _vp(stream or None)))
+
+
+class KeySwitch:
+    """HYBRID key switching for ring 2**log_n, ciphertext moduli q (with roots
+    rq), special moduli p (roots rp) and num_part_q digits."""
+
+    def __init__(self, ctx: Context, log_n: int, q: Sequence[int], rq: Sequence[int], p: Sequence[int],
+                 rp: Sequence[int], num_part_q: int):
+        self.ctx = ctx
+        self.log_n, self.n = int(log_n), 1 << int(log_n)
+        self.q, self.p = [int(v) for v in q], [int(v) for v in p]
+        self.size_q, self.size_p = len(self.q), len(self.p)
+        self.num_part_q = int(num_part_q)
+        h = _vp()
+        _check(lib().ofhe_hip_ks_create(ctx.handle, self.log_n, self.size_q, _arr(q), _arr(rq), self.size_p,
+                                        _arr(p), _arr(rp), self.num_part_q, ctypes.byref(h)))
+        self._h = h
+
+    def close(self) -> None:
+        if self._h is not None:
+            _check(lib().ofhe_hip_ks_destroy(self._h))
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def digits(self, size_ql: int):
+        """(alpha, beta) at level size_ql."""
+        a, b = ctypes.c_uint32(0), ctypes.c_uint32(0)
+        _check(lib().ofhe_hip_ks_digits(self._h, int(size_ql), ctypes.byref(a), ctypes.byref(b)))
+        return a.value, b.value
+
+    def precompute(self, size_ql: int, c: int, digits: int, batch: int = 1, stream: int = 0) -> None:
+        _check(lib().ofhe_hip_ks_precompute(self._h, int(size_ql), _vp(c), _vp(digits), int(batch),
+                                            _vp(stream or None)))
+
+    def fast_core_ext(self, size_ql: int, digits: int, key_b: int, key_a: int, ct0: int, ct1: int,
+                      batch: int = 1, stream: int = 0) -> None:
+        _check(lib().ofhe_hip_ks_fast_core_ext(self._h, int(size_ql), _vp(digits), _vp(key_b), _vp(key_a),
+                                               _vp(ct0), _vp(ct1), int(batch), _vp(stream or None)))
+
+    def mod_down(self, size_ql: int, x: int, out: int, t: int = 0, batch: int = 1, stream: int = 0) -> None:
+        _check(lib().ofhe_hip_ks_mod_down(self._h, int(size_ql), _vp(x), _vp(out), int(t), int(batch),
+                                          _vp(stream or None)))
+
+    def core(self, size_ql: int, c: int, key_b: int, key_a: int, out0: int, out1: int, t: int = 0,
+             batch: int = 1, stream: int = 0) -> None:
+        _check(lib().ofhe_hip_ks_core(self._h, int(size_ql), _vp(c), _vp(key_b), _vp(key_a), _vp(out0),
+                                      _vp(out1), int(t), int(batch), _vp(stream or None)))
