@@ -92,7 +92,13 @@ def main():
     ap.add_argument("--batch", type=int, default=1024, help="polynomials per GPU")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget (0 = skip)")
     ap.add_argument("--no-check", action="store_true")
+    ap.add_argument("--workload", default="pipeline", choices=["pipeline", "keyswitch"],
+                    help="pipeline = the headline metric (configs[2]); keyswitch = configs[4] HYBRID "
+                         "key switching (secondary line, not the headline)")
+    ap.add_argument("--ks-batch", type=int, default=8, help="ciphertext polynomials per GPU (keyswitch)")
     args = ap.parse_args()
+    if args.workload == "keyswitch":
+        return bench_keyswitch(args)
 
     import torch
     import torch.distributed as dist
@@ -266,6 +272,118 @@ def main():
             "cpu_baseline": cpu,
             "parity_spot_check": parity,
             "evalkey_broadcast": bcast,
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def bench_keyswitch(args):
+    """configs[4]: N = 2^17, 48 Q towers, dnum = 3, P = 16 towers; KeySwitchCore
+    (ModUp -> key inner product -> 2x ModDown) on a batch of ciphertext
+    polynomials per GPU, weak-scaled by batch.  Prints one JSON line."""
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+    import ofhe_hip as H
+    import shard
+
+    log_n, sq, sp, dnum = 17, 48, 16, 3
+    n = 1 << log_n
+    allq, allr = moduli_chain(log_n, sq + sp)
+    q, rq, p, rp = allq[:sq], allr[:sq], allq[sq:], allr[sq:]
+    B = args.ks_batch
+    ctx = H.Context(local)
+    ks = H.KeySwitch(ctx, log_n, q, rq, p, rp, dnum)
+    _, beta = ks.digits(sq)
+    g = torch.Generator(device=dev)
+    g.manual_seed(0x5EED + rank)
+
+    def uniform(shape, moduli):
+        x = torch.empty(shape, dtype=torch.int64, device=dev)
+        for t, m in enumerate(moduli):
+            x[..., t, :].random_(0, m, generator=g)
+        return x
+
+    c = uniform((B, sq, n), q)
+    kb = torch.empty((dnum, sq + sp, n), dtype=torch.int64, device=dev)
+    ka = torch.empty_like(kb)
+    if rank == 0 or world == 1:
+        kb.copy_(uniform((dnum, sq + sp, n), q + p))
+        ka.copy_(uniform((dnum, sq + sp, n), q + p))
+    if world > 1:  # the evaluation key comes from rank 0 over RCCL (configs[3]/[4])
+        shard.broadcast_evalkey(kb, src=0)
+        shard.broadcast_evalkey(ka, src=0)
+    o0 = torch.empty((B, sq, n), dtype=torch.int64, device=dev)
+    o1 = torch.empty_like(o0)
+    digits = torch.empty((B, beta, sq + sp, n), dtype=torch.int64, device=dev)
+    ct = torch.empty((2, B, sq + sp, n), dtype=torch.int64, device=dev)
+    st = torch.cuda.current_stream(dev)
+    sptr = st.cuda_stream
+
+    def step():
+        ks.core(sq, c.data_ptr(), kb.data_ptr(), ka.data_ptr(), o0.data_ptr(), o1.data_ptr(), 0, B, sptr)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        elapsed = shard.max_over_ranks(elapsed, device=dev)
+    # stage split with events on the launch stream
+    stages = {}
+    reps = max(2, min(args.steps, 5))
+    calls = {
+        "mod_up(precompute)": lambda: ks.precompute(sq, c.data_ptr(), digits.data_ptr(), B, sptr),
+        "inner_product": lambda: ks.fast_core_ext(sq, digits.data_ptr(), kb.data_ptr(), ka.data_ptr(),
+                                                  ct[0].data_ptr(), ct[1].data_ptr(), B, sptr),
+        "mod_down(x2)": lambda: (ks.mod_down(sq, ct[0].data_ptr(), o0.data_ptr(), 0, B, sptr),
+                                 ks.mod_down(sq, ct[1].data_ptr(), o1.data_ptr(), 0, B, sptr)),
+    }
+    for name, fn in calls.items():
+        fn()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(st)
+        for _ in range(reps):
+            fn()
+        e1.record(st)
+        e1.synchronize()
+        stages[name] = e0.elapsed_time(e1) / reps
+    # minimum HBM words per ciphertext polynomial and tower-coefficient: read c
+    # (Q), write + read the digits (2 beta (Q+P)), write ct0/ct1 (2 (Q+P)),
+    # ModDown reads them (2 (Q+P)) and writes out0/out1 (2 Q); keys are shared
+    # by the batch and not counted (DESIGN.md)
+    qp = sq + sp
+    alg_words = sq + 2 * beta * qp + 4 * qp + 2 * sq
+    value = B * world * args.steps / elapsed
+    if rank == 0:
+        out = {
+            "metric": "HYBRID key switches/sec (KeySwitchCore), N=2^17, 48+16 towers, dnum=3",
+            "value": value, "unit": "keyswitch/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "u64", "data": "synthetic: uniform ciphertext and key residues",
+            "config": {"workload": "configs[4]: N=2^17, Q=48, P=16, dnum=3, KeySwitchCore",
+                       "batch_per_gpu": B, "global_batch": B * world,
+                       "parallelism": f"ciphertext-batch-sharded x{world}, key broadcast over RCCL"},
+            "stages_ms": stages,
+            "alg_hbm_gbs": alg_words * 8 * n * B / (elapsed / args.steps) / 1e9,
         }
         print(json.dumps(out), flush=True)
     if world > 1:

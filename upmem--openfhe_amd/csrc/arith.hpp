@@ -39,7 +39,19 @@ __device__ __forceinline__ u64 csub(u64 x, u64 m) { return x >= m ? x - m : x; }
 
 // floor(a*b / 2^64) - e, e in {0, 1, 2}: drops a0*b0 and the carry of the
 // middle sum.
+#ifndef OFHE_QH_ADDC
+#define OFHE_QH_ADDC 0  // measured: more instructions (add_co + cndmask), kept for reference
+#endif
 __device__ __forceinline__ u64 mulhi_approx(u64 a, u64 b) {
+    if (OFHE_QH_ADDC) {
+        // the two middle high words summed with an explicit carry word, so the
+        // 64-bit accumulator is built by add/carry instead of zero-extending
+        // moves plus a 64-bit add
+        const u32 h1 = __umulhi(lo32(a), hi32(b));
+        const u32 h2 = __umulhi(hi32(a), lo32(b));
+        const u32 s = h1 + h2;
+        return mad32(hi32(a), hi32(b), pack(s, s < h1));
+    }
     const u64 m1 = mad32(lo32(a), hi32(b), 0);
     const u64 m2 = mad32(hi32(a), lo32(b), 0);
     return mad32(hi32(a), hi32(b), (m1 >> 32) + (m2 >> 32));
@@ -64,6 +76,7 @@ template <bool SPQ>
 struct Mod {
     u64 q;    // modulus, q < 2^60
     u64 q4;   // 4q
+    u64 q8;   // 8q
     u64 nq;   // 2^64 - q   (loaded, not derived, so LLVM keeps the adds)
     u64 nq4;  // 2^64 - 4q
     u32 sh;   // L - 32 (SPQ only)
@@ -88,7 +101,7 @@ __device__ __forceinline__ u64 shoup_lazy(u64 a, u64 w, u64 wp, const Mod<SPQ>& 
 
 // canonical Shoup: ModMulFastConstEq semantics (result in [0, q)), generic q.
 __device__ __forceinline__ u64 shoup_canon(u64 a, u64 w, u64 wp, u64 q) {
-    const Mod<false> M{q, 4 * q, 0 - q, 0 - 4 * q, 0};
+    const Mod<false> M{q, 4 * q, 8 * q, 0 - q, 0 - 4 * q, 0};
     u64 r = shoup_lazy(a, w, wp, M);
     r = csub(r, 2 * q);
     return csub(r, q);

@@ -41,7 +41,7 @@ struct TowerConst {
 };
 template <bool SPQ>
 __device__ __forceinline__ Mod<SPQ> load_mod(const TowerConst& tc) {
-    return Mod<SPQ>{tc.q, 4 * tc.q, tc.nq, tc.nq4, tc.spq_sh};
+    return Mod<SPQ>{tc.q, 4 * tc.q, 8 * tc.q, tc.nq, tc.nq4, tc.spq_sh};
 }
 
 // Device view of a plan. Twiddles are interleaved (w, w') pairs so one
@@ -74,13 +74,27 @@ __device__ __forceinline__ Tw ldtw(const u64* base, u32 idx) {
     return Tw{v.x, v.y};
 }
 
-// Cooley-Tukey butterfly, inputs in [0, 8q), outputs in [0, 8q).
+// Cooley-Tukey butterfly.  Two lazy-reduction schemes (OFHE_LAZY_FWD):
+//  0: every stage subtracts 4q from x when x >= 4q; values stay in [0, 8q).
+//  1: stages alternate.  A "CS" stage (odd stage of a radix-16 round, the
+//     last stage of a column pass) subtracts 8q when x >= 8q and maps
+//     [0, 16q) -> [0, 12q); the other stages skip the conditional subtract and
+//     map [0, 12q) -> [0, 16q).  16q <= 2^64 because q < 2^60, and shoup_lazy
+//     accepts any 64-bit input, so half of the butterflies save the compare,
+//     two selects and the 64-bit subtract.
+#ifndef OFHE_LAZY_FWD
+#define OFHE_LAZY_FWD 1
+#endif
 template <class M_>
-__device__ __forceinline__ void ct_bfly(u64& x, u64& y, Tw w, const M_& M) {
+__device__ __forceinline__ void ct_bfly_cs(u64& x, u64& y, Tw w, const M_& M, bool cs) {
     const u64 t = shoup_lazy(y, w.w, w.wp, M);  // [0, 4q)
-    const u64 a = csub(x, M.q4);                // [0, 4q)
+    const u64 a = OFHE_LAZY_FWD ? (cs ? csub(x, M.q8) : x) : csub(x, M.q4);
     x = a + t;
     y = a + M.q4 - t;
+}
+template <int CS, class M_>
+__device__ __forceinline__ void ct_bfly(u64& x, u64& y, Tw w, const M_& M) {
+    ct_bfly_cs(x, y, w, M, CS != 0);
 }
 
 // Gentleman-Sande butterfly, inputs in [0, 4q), outputs in [0, 4q).
@@ -106,6 +120,11 @@ __device__ __forceinline__ u64 canon8(u64 x, u64 q) {  // [0, 8q) -> [0, q)
     x = csub(x, 2 * q);
     return csub(x, q);
 }
+// forward-transform output (any stage pattern) -> [0, q)
+__device__ __forceinline__ u64 canon_fwd(u64 x, u64 q) {
+    if (OFHE_LAZY_FWD) x = csub(x, 8 * q);  // [0, 16q) -> [0, 8q)
+    return canon8(x, q);
+}
 __device__ __forceinline__ u64 canon4(u64 x, u64 q) {  // [0, 4q) -> [0, q)
     x = csub(x, 2 * q);
     return csub(x, q);
@@ -125,7 +144,7 @@ __device__ __forceinline__ void fwd_stage16(u64 (&v)[16], const u64* tw, u32 M0,
     for (int j = 0; j < (1 << S); j++) {
         Tw w = ldtw(base, j);
 #pragma unroll
-        for (int k = j * 2 * half; k < j * 2 * half + half; k++) ct_bfly(v[k], v[k + half], w, M);
+        for (int k = j * 2 * half; k < j * 2 * half + half; k++) ct_bfly<S & 1>(v[k], v[k + half], w, M);
     }
 }
 
@@ -239,7 +258,7 @@ __global__ __launch_bounds__(256, OFHE_KB_WAVES) void k_block(PlanArgs P, const 
         for (int k = 0; k < 16; k++) v[k] = lds[L3 + k];
         fwd_round16(v, tw, (N >> 4) + g * 256 + tid, M);
 #pragma unroll
-        for (int k = 0; k < 16; k++) v[k] = canon8(v[k], q);
+        for (int k = 0; k < 16; k++) v[k] = canon_fwd(v[k], q);
         if (MODE == MODE_FWD) {
             ulonglong2* o = reinterpret_cast<ulonglong2*>(oblk + tid * 16);
 #pragma unroll
@@ -375,7 +394,7 @@ __device__ __forceinline__ void cols_fwd(u64 (&v)[CPT][E], const u64* tw, const 
 #pragma unroll
             for (int k = j * 2 * half; k < j * 2 * half + half; k++)
 #pragma unroll
-                for (int c = 0; c < CPT; c++) ct_bfly(v[c][k], v[c][k + half], w, M);
+                for (int c = 0; c < CPT; c++) ct_bfly_cs(v[c][k], v[c][k + half], w, M, ((KA - 1 - s) & 1) == 0);
         }
     }
 }
@@ -467,14 +486,14 @@ __global__ __launch_bounds__(256) void k_small(PlanArgs P, const u64* src, u64* 
             for (u32 k = threadIdx.x; k < half; k += blockDim.x) {
                 const u32 i = k >> lt, j = (i << (lt + 1)) + (k & (tt - 1));
                 u64 x = lds[j], y = lds[j + tt];
-                ct_bfly(x, y, ldtw(tw, m + i), M);
+                ct_bfly<1>(x, y, ldtw(tw, m + i), M);
                 lds[j] = x;
                 lds[j + tt] = y;
             }
             __syncthreads();
         }
         for (u32 i = threadIdx.x; i < N; i += blockDim.x) {
-            u64 x = canon8(lds[i], q);
+            u64 x = canon_fwd(lds[i], q);
             if (MODE == MODE_FUSED) x = barrett_ref(x, bdat[off + i], q, tc.mu, tc.nshift);
             lds[i] = x;
         }
