@@ -58,6 +58,7 @@ struct BconvArgs {
     const u64* qv;        // [sizeQ]
     const u64* qhinv;     // [sizeQ][2]  (QHatInvModq, Shoup precon)
     const u64* qhmodp;    // [sizeQ][sizeP]
+    const u64* qhlimb;    // [sizeQ][sizeP rounded up to BCONV_PT], (c mod 2^30) | (c >> 30) << 32, zero padded
     const u64* pv;        // [sizeP]
     const u64* pmu;       // [sizeP][2]  (mu_lo, mu_hi) = floor(2^128 / p)
     u64 in_stride;        // words between batch entries of x   (sizeQ * N when dense)
@@ -100,6 +101,74 @@ __global__ __launch_bounds__(256) void k_bconv(BconvArgs A, const u64* __restric
                 const u32 jj = j0 + j;
                 const u32 jo = jj >= A.gap_at ? jj + A.gap : jj;
                 ob[(u64)jo * N] = barrett128(lo[j], hi[j], A.pv[jj], A.pmu[2 * jj], A.pmu[2 * jj + 1]);
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Limb variant (any size_q <= 16).  y_i is split into two 30-bit limbs and
+// every QHatModp entry c < 2^60 is pre-split the same way, so
+//   sum_i y_i c_ij = A0 + (A1 + A2) 2^30 + A3 2^60,
+//   A0 = sum y0 c0, A1 = sum y0 c1, A2 = sum y1 c0, A3 = sum y1 c1,
+// where every A is a sum of at most 16 products below 2^60: four
+// v_mad_u64_u32 per term and no carry handling (mul128 plus a 128-bit add
+// needs the same four multiplies and the carries).  The 128-bit total is
+// reduced with the same BarrettUint128ModUint64, so the output is the same
+// canonical value.  The limb table is zero-padded to a multiple of PT
+// columns so the inner loop has no branches.
+// ---------------------------------------------------------------------------
+constexpr u32 LIMB = 30;
+constexpr u64 LIMB_MASK = (1ull << LIMB) - 1;
+constexpr u32 BCONV_PT = 8;      // output towers per tile
+constexpr u32 BCONV_LIMB_QMAX = 16;
+
+__device__ __forceinline__ void limbs_to_u128(u64 a0, u64 a1, u64 a2, u64 a3, u64& lo, u64& hi) {
+    const u64 m = a1 + a2;
+    const u64 mc = m < a1;  // carry of the middle sum (weight 2^94)
+    lo = a0 + (m << LIMB);
+    u64 c = lo < a0;
+    const u64 t = a3 << (2 * LIMB);
+    lo += t;
+    c += lo < t;
+    hi = (m >> (64 - LIMB)) + (mc << LIMB) + (a3 >> (64 - 2 * LIMB)) + c;
+}
+
+template <int PT>
+__global__ __launch_bounds__(256) void k_bconv_limb(BconvArgs A, const u64* __restrict__ x, u64* __restrict__ out,
+                                                    u32 batch) {
+    const u32 N = 1u << A.log_n;
+    const u64 gid = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (gid >= (u64)batch * N) return;
+    const u32 b = (u32)(gid >> A.log_n), ri = (u32)(gid & (N - 1));
+    const u64* xb = x + (u64)b * A.in_stride + ri;
+    u64* ob = out + (u64)b * A.out_stride + ri;
+    const u32 ppad = (A.size_p + PT - 1) / PT * PT;
+    for (u32 j0 = 0; j0 < A.size_p; j0 += PT) {
+        u64 a0[PT], a1[PT], a2[PT], a3[PT];
+#pragma unroll
+        for (int j = 0; j < PT; j++) a0[j] = a1[j] = a2[j] = a3[j] = 0;
+        for (u32 i = 0; i < A.size_q; i++) {
+            const u64 y = shoup_canon(xb[(u64)i * N], A.qhinv[2 * i], A.qhinv[2 * i + 1], A.qv[i]);
+            const u32 y0 = (u32)(y & LIMB_MASK), y1 = (u32)(y >> LIMB);
+            const u64* cl = A.qhlimb + (u64)i * ppad + j0;
+#pragma unroll
+            for (int j = 0; j < PT; j++) {
+                const u64 c = cl[j];
+                a0[j] = mad32(y0, lo32(c), a0[j]);
+                a1[j] = mad32(y0, hi32(c), a1[j]);
+                a2[j] = mad32(y1, lo32(c), a2[j]);
+                a3[j] = mad32(y1, hi32(c), a3[j]);
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < PT; j++) {
+            const u32 jj = j0 + j;
+            if (jj < A.size_p) {
+                u64 lo, hi;
+                limbs_to_u128(a0[j], a1[j], a2[j], a3[j], lo, hi);
+                const u32 jo = jj >= A.gap_at ? jj + A.gap : jj;
+                ob[(u64)jo * N] = barrett128(lo, hi, A.pv[jj], A.pmu[2 * jj], A.pmu[2 * jj + 1]);
             }
         }
     }

@@ -416,10 +416,18 @@ int ofhe_hip_ks_fast_core_ext(ofhe_ks_t k, uint32_t size_ql, const uint64_t* dig
     KsLevel* L = nullptr;
     RCCHK(level_get(k, size_ql, &L));
     const u32 towers = size_ql + k->size_p;
-    const u64 npairs = ((u64)batch * towers << k->log_n) / 2;
     const u64 key_stride = (u64)(k->size_q + k->size_p) << k->log_n;
-    hipLaunchKernelGGL(k_ks_inner, dim3(grid_for(npairs)), dim3(256), 0, pick(stream), L->d_tow, digits, key_b, key_a,
-                       ct0, ct1, key_stride, L->beta, npairs, k->log_n, towers);
+    if (L->beta <= 4) {
+        // batch-stationary keys: one thread per (tower, coefficient pair)
+        const u64 rows = ((u64)towers << k->log_n) / 2;
+        const u64 blocks = (rows + 255) / 256;
+        hipLaunchKernelGGL(k_ks_inner_bs<4>, dim3((u32)blocks), dim3(256), 0, pick(stream), L->d_tow, digits, key_b,
+                           key_a, ct0, ct1, key_stride, L->beta, batch, rows, k->log_n, towers);
+    } else {
+        const u64 npairs = ((u64)batch * towers << k->log_n) / 2;
+        hipLaunchKernelGGL(k_ks_inner, dim3(grid_for(npairs)), dim3(256), 0, pick(stream), L->d_tow, digits, key_b,
+                           key_a, ct0, ct1, key_stride, L->beta, npairs, k->log_n, towers);
+    }
     return post_launch();
 }
 

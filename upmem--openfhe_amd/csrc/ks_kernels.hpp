@@ -112,6 +112,66 @@ __global__ __launch_bounds__(256) void k_ks_inner(const KsTower* __restrict__ tw
     }
 }
 
+// Same product, batch-stationary keys: a thread owns (tower, coefficient
+// pair) and walks the batch, so each key word is read once per launch instead
+// of once per ciphertext.  Sums use the 30-bit limb split of k_bconv_limb
+// (beta <= 16 terms below 2^60 per limb sum).  Digits j >= beta are masked by
+// zero key limbs, keeping the loop branch-free.
+template <int BMAX>
+__global__ __launch_bounds__(256) void k_ks_inner_bs(const KsTower* __restrict__ tw, const u64* __restrict__ digits,
+                                                     const u64* __restrict__ kb, const u64* __restrict__ ka,
+                                                     u64* __restrict__ ct0, u64* __restrict__ ct1, u64 key_stride,
+                                                     u32 beta, u32 batch, u64 npairs_row, u32 log_n, u32 towers) {
+    const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= npairs_row) return;
+    const u64 e = 2 * i;
+    const u32 t = (u32)(e >> log_n), c = (u32)(e & ((1ull << log_n) - 1));
+    const KsTower T = tw[t];
+    const u64 poly = (u64)towers << log_n;
+    const u64 inner = ((u64)t << log_n) + c;
+    u64 kl[BMAX][4];  // (b.x, b.y, a.x, a.y) as (lo30 | hi30 << 32)
+#pragma unroll
+    for (int j = 0; j < BMAX; j++) {
+        const bool on = j < (int)beta;
+        const u64 off = T.key_off + c + (u64)(on ? j : 0) * key_stride;
+        const ulonglong2 vb = *reinterpret_cast<const ulonglong2*>(kb + off);
+        const ulonglong2 va = *reinterpret_cast<const ulonglong2*>(ka + off);
+        const u64 w[4] = {vb.x, vb.y, va.x, va.y};
+#pragma unroll
+        for (int k = 0; k < 4; k++) kl[j][k] = on ? ((w[k] & LIMB_MASK) | ((w[k] >> LIMB) << 32)) : 0;
+    }
+    for (u32 b = 0; b < batch; b++) {
+        const u64* d = digits + (u64)b * beta * poly + inner;
+        u64 acc[4][4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) acc[k][0] = acc[k][1] = acc[k][2] = acc[k][3] = 0;
+#pragma unroll
+        for (int j = 0; j < BMAX; j++) {
+            const ulonglong2 x = *reinterpret_cast<const ulonglong2*>(d + (u64)(j < (int)beta ? j : 0) * poly);
+            const u32 x0[2] = {(u32)(x.x & LIMB_MASK), (u32)(x.y & LIMB_MASK)};
+            const u32 x1[2] = {(u32)(x.x >> LIMB), (u32)(x.y >> LIMB)};
+#pragma unroll
+            for (int k = 0; k < 4; k++) {  // k: (ct0, coef 0), (ct0, 1), (ct1, 0), (ct1, 1)
+                const u64 kw = kl[j][k];
+                acc[k][0] = mad32(x0[k & 1], lo32(kw), acc[k][0]);
+                acc[k][1] = mad32(x0[k & 1], hi32(kw), acc[k][1]);
+                acc[k][2] = mad32(x1[k & 1], lo32(kw), acc[k][2]);
+                acc[k][3] = mad32(x1[k & 1], hi32(kw), acc[k][3]);
+            }
+        }
+        u64 r[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            u64 lo, hi;
+            limbs_to_u128(acc[k][0], acc[k][1], acc[k][2], acc[k][3], lo, hi);
+            r[k] = barrett128(lo, hi, T.m, T.mu_lo, T.mu_hi);
+        }
+        const u64 o = (u64)b * poly + inner;
+        *reinterpret_cast<ulonglong2*>(ct0 + o) = make_ulonglong2(r[0], r[1]);
+        *reinterpret_cast<ulonglong2*>(ct1 + o) = make_ulonglong2(r[2], r[3]);
+    }
+}
+
 // NativeVectorT::SwitchModulus (mubintvecnat.cpp:111-136), value for value.
 __global__ __launch_bounds__(256) void k_switch_modulus(const u64* src, u64* dst, u64 n, u64 om, u64 nm) {
     const u64 step = (u64)gridDim.x * blockDim.x;

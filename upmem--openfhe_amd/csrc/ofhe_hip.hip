@@ -594,8 +594,9 @@ int ofhe_hip_bconv_create(ofhe_ctx_t ctx, uint32_t log_n, uint32_t size_q, uint3
         if (q[i] < 2 || q[i] >= (1ull << 60)) return fail(OFHE_ERR_ARG, "q out of range");
     for (u32 j = 0; j < size_p; j++)
         if (p[j] < 2 || p[j] >= (1ull << 60)) return fail(OFHE_ERR_ARG, "p out of range");
-    // layout: qv[Q] | qhinv[2Q] | qhmodp[Q*P] | pv[P] | pmu[2P]
-    const size_t words = size_q + 2 * size_q + (size_t)size_q * size_p + size_p + 2 * size_p;
+    // layout: qv[Q] | qhinv[2Q] | qhmodp[Q*P] | pv[P] | pmu[2P] | qhlimb[Q*Ppad]
+    const u32 ppad = (size_p + BCONV_PT - 1) / BCONV_PT * BCONV_PT;
+    const size_t words = size_q + 2 * size_q + (size_t)size_q * size_p + size_p + 2 * size_p + (size_t)size_q * ppad;
     std::vector<u64> h(words);
     u64* qv = h.data();
     u64* qhinv = qv + size_q;
@@ -607,7 +608,13 @@ int ofhe_hip_bconv_create(ofhe_ctx_t ctx, uint32_t log_n, uint32_t size_q, uint3
         qhinv[2 * i] = qhat_inv_modq[i] % q[i];
         qhinv[2 * i + 1] = shoup_pre(qhinv[2 * i], q[i]);
     }
-    memcpy(qhmodp, qhat_modp, sizeof(u64) * size_q * size_p);
+    u64* qhlimb = pmu + 2 * size_p;
+    for (u32 i = 0; i < size_q; i++)
+        for (u32 j = 0; j < size_p; j++) {
+            const u64 c = qhat_modp[(size_t)i * size_p + j] % p[j];
+            qhmodp[(size_t)i * size_p + j] = c;
+            qhlimb[(size_t)i * ppad + j] = (c & LIMB_MASK) | ((c >> LIMB) << 32);
+        }
     for (u32 j = 0; j < size_p; j++) {
         pv[j] = p[j];
         const u128 mu = (~(u128)0) / p[j];  // floor(2^128 / p), p odd
@@ -631,6 +638,7 @@ int ofhe_hip_bconv_create(ofhe_ctx_t ctx, uint32_t log_n, uint32_t size_q, uint3
     A.qhmodp = A.qhinv + 2 * size_q;
     A.pv = A.qhmodp + (size_t)size_q * size_p;
     A.pmu = A.pv + size_p;
+    A.qhlimb = A.pmu + 2 * size_p;
     A.log_n = log_n;
     A.size_q = size_q;
     A.size_p = size_p;
@@ -655,7 +663,11 @@ int bconv_run(const BconvArgs& A, const u64* x, u64* out, u32 batch, hipStream_t
     const u64 total = (u64)batch << A.log_n;
     const u64 blocks = (total + 255) / 256;
     if (blocks >= (1ull << 31)) return fail(OFHE_ERR_ARG, "batch too large");
-    hipLaunchKernelGGL((k_bconv<8>), dim3((u32)blocks), dim3(256), 0, s, A, x, out, batch);
+    static const bool generic = getenv("OFHE_BCONV_GENERIC") != nullptr;  // A/B switch
+    if (A.size_q <= BCONV_LIMB_QMAX && !generic)
+        hipLaunchKernelGGL((k_bconv_limb<BCONV_PT>), dim3((u32)blocks), dim3(256), 0, s, A, x, out, batch);
+    else
+        hipLaunchKernelGGL((k_bconv<8>), dim3((u32)blocks), dim3(256), 0, s, A, x, out, batch);
     return post_launch();
 }
 }  // namespace ofhe
