@@ -57,7 +57,7 @@ for t, q in enumerate(qs):
 c = torch.empty_like(a)
 s = torch.cuda.current_stream()
 sp = vp(s.cuda_stream)
-times = {nm: {0: [], 1: [], 2: [], "all": []} for nm, _, _ in libs}
+times = {nm: {0: [], 1: [], 2: [], "all": [], "fwd": [], "inv": []} for nm, _, _ in libs}
 ref = None
 for rnd in range(int(os.environ.get("EXP_ROUNDS", "6"))):
     for nm, L, plan in libs:
@@ -79,6 +79,17 @@ for rnd in range(int(os.environ.get("EXP_ROUNDS", "6"))):
             e1.synchronize()
             if rnd > 0:
                 times[nm][st].append(e0.elapsed_time(e1))
+        # standalone forward / inverse transforms (FWD / INV block modes)
+        for st in ("fwd", "inv"):
+            x = a.clone()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(s)
+            fn = L.ofhe_hip_ntt_fwd if st == "fwd" else L.ofhe_hip_ntt_inv
+            assert fn(plan, vp(x.data_ptr()), B, sp) == 0
+            e1.record(s)
+            e1.synchronize()
+            if rnd > 0:
+                times[nm][st].append(e0.elapsed_time(e1))
         if ref is None:
             ref = c.clone()
         elif not torch.equal(ref, c):
@@ -88,4 +99,5 @@ for nm in times:
     tt = times[nm]
     med = {k: statistics.median(v) for k, v in tt.items()}
     print(f"{nm:44s} cols_f {med[0]:7.3f} block {med[1]:7.3f} cols_i {med[2]:7.3f} all {med['all']:7.3f} ms "
-          f"-> {coeffs / med['all'] * 1e3:.3e} coeffs/s (min all {min(tt['all']):.3f})", flush=True)
+          f"-> {coeffs / med['all'] * 1e3:.3e} coeffs/s (min all {min(tt['all']):.3f}) "
+          f"| ntt fwd {med['fwd']:7.3f} inv {med['inv']:7.3f} ms", flush=True)

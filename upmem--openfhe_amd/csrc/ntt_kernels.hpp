@@ -51,6 +51,8 @@ struct PlanArgs {
     const u64* tw;         // [T][N][2]   forward Table (bit-reversed powers of psi)
     const u64* itw;        // [T][N][2]   inverse TableI
     const u64* itwn;       // [T][N/2][2] TableI[N/2 + i] * N^-1 (first inverse stage)
+    const u64* tw3;        // [T][15N/16][2] round-3 forward twiddles, lane-contiguous (log_n >= 12)
+    const u64* itw3;       // [T][15N/16][2] round-3 inverse twiddles (stage t = 1 with N^-1)
     u64 sstride;           // words between batch entries of src (towers * N when dense)
     u64 dstride;           // words between batch entries of dst (and of the Hadamard operand)
     u32 log_n;
@@ -188,6 +190,59 @@ __device__ __forceinline__ void inv_round16(u64 (&v)[16], const u64* itw, u32 M0
     inv_stage16<0>(v, itw, M0, M);
 }
 
+// ---------------------------------------------------------------------------
+// Round 3 of k_block (st = 1) gives every thread its own twiddles: thread u
+// of the block's 256 (global u = 256 g + tid, M0 = N/16 + u) needs
+// Table[(M0 << S) + j], j < 2^S.  Read from Table directly, lanes are 2^S
+// entries apart and one wave-wide 16-byte load touches 64 cache lines.  The
+// plan therefore also stores these twiddles transposed, tw3[S][j][u] at
+// ((2^S - 1) U + j U + u) with U = N/16, so a wave reads 1 KiB contiguous per
+// load, from a uniform (scalar) base plus the lane offset.
+// ---------------------------------------------------------------------------
+#ifndef OFHE_TW3
+#define OFHE_TW3 1
+#endif
+// k_block's round-3 layout gives each thread 16 consecutive words, so direct
+// global access is one 128-byte line per lane per instruction.  With
+// OFHE_COAL the block's Hadamard operand, inverse input and forward output go
+// through LDS in the coalesced round-1 layout instead.
+#ifndef OFHE_COAL
+#define OFHE_COAL 1
+#endif
+// Staging the Hadamard operand the same way costs two more barriers in the
+// fused kernel and measured 6 % slower there, so it is off.
+#ifndef OFHE_COAL_B
+#define OFHE_COAL_B 0
+#endif
+template <int S, class M_>
+__device__ __forceinline__ void fwd_stage16_t3(u64 (&v)[16], const u64* tw3, u32 U, u32 u, const M_& M) {
+    constexpr int half = 8 >> S;
+    const u64* base = tw3 + 2 * (u64)(((1u << S) - 1) * U);
+#pragma unroll
+    for (int j = 0; j < (1 << S); j++) {
+        Tw w = ldtw(base + 2 * (u64)j * U, u);
+#pragma unroll
+        for (int k = j * 2 * half; k < j * 2 * half + half; k++) ct_bfly<S & 1>(v[k], v[k + half], w, M);
+    }
+}
+template <int S, class M_>
+__device__ __forceinline__ void inv_stage16_t3(u64 (&v)[16], const u64* itw3, u32 U, u32 u, const TowerConst& tc,
+                                               const M_& M) {
+    constexpr int half = 8 >> S;
+    const u64* base = itw3 + 2 * (u64)(((1u << S) - 1) * U);
+#pragma unroll
+    for (int j = 0; j < (1 << S); j++) {
+        Tw w = ldtw(base + 2 * (u64)j * U, u);
+#pragma unroll
+        for (int k = j * 2 * half; k < j * 2 * half + half; k++) {
+            if (S == 3)
+                gs_bfly_ninv(v[k], v[k + half], w, tc.ninv, tc.ninv_pre, M);
+            else
+                gs_bfly(v[k], v[k + half], w, M);
+        }
+    }
+}
+
 // LDS placement of block element p: one u64 of padding per 16 elements.  It is
 // additive, so every round addresses its 16 values as one base register plus
 // immediate offsets, and it is bank-conflict free for the round-2/3 patterns
@@ -256,35 +311,78 @@ __global__ __launch_bounds__(256, OFHE_KB_WAVES) void k_block(PlanArgs P, const 
         // round 3: st = 1, p = 16 tid + k
 #pragma unroll
         for (int k = 0; k < 16; k++) v[k] = lds[L3 + k];
-        fwd_round16(v, tw, (N >> 4) + g * 256 + tid, M);
+        if (OFHE_TW3) {
+            const u64* tw3 = P.tw3 + (u64)t * (N / 16) * 30;
+            const u32 U = N >> 4, u = g * 256 + tid;
+            fwd_stage16_t3<0>(v, tw3, U, u, M);
+            fwd_stage16_t3<1>(v, tw3, U, u, M);
+            fwd_stage16_t3<2>(v, tw3, U, u, M);
+            fwd_stage16_t3<3>(v, tw3, U, u, M);
+        } else {
+            fwd_round16(v, tw, (N >> 4) + g * 256 + tid, M);
+        }
 #pragma unroll
         for (int k = 0; k < 16; k++) v[k] = canon_fwd(v[k], q);
         if (MODE == MODE_FWD) {
-            ulonglong2* o = reinterpret_cast<ulonglong2*>(oblk + tid * 16);
+            if (OFHE_COAL) {
+                // own L3 slots were this thread's round-3 inputs: no hazard
 #pragma unroll
-            for (int k = 0; k < 8; k++) o[k] = make_ulonglong2(v[2 * k], v[2 * k + 1]);
+                for (int k = 0; k < 16; k++) lds[L3 + k] = v[k];
+                __syncthreads();
+#pragma unroll
+                for (int k = 0; k < 16; k++) oblk[tid + 256 * k] = lds[L1 + 272 * k];
+            } else {
+                ulonglong2* o = reinterpret_cast<ulonglong2*>(oblk + tid * 16);
+#pragma unroll
+                for (int k = 0; k < 8; k++) o[k] = make_ulonglong2(v[2 * k], v[2 * k + 1]);
+            }
             return;
         }
         // Hadamard with b (evaluation form), NativeVectorT::ModMulNoCheckEq
-        const ulonglong2* bp = reinterpret_cast<const ulonglong2*>(bdat + off + tid * 16);
+        if (OFHE_COAL_B) {
+            // b staged through LDS: coalesced rows in, this thread's 16 out
+            __syncthreads();  // every thread has read its round-3 inputs
 #pragma unroll
-        for (int k = 0; k < 8; k++) {
-            ulonglong2 bb = bp[k];
-            v[2 * k] = barrett_ref(v[2 * k], bb.x, q, tc.mu, tc.nshift);
-            v[2 * k + 1] = barrett_ref(v[2 * k + 1], bb.y, q, tc.mu, tc.nshift);
+            for (int k = 0; k < 16; k++) lds[L1 + 272 * k] = bdat[off + tid + 256 * k];
+            __syncthreads();
+#pragma unroll
+            for (int k = 0; k < 16; k++) v[k] = barrett_ref(v[k], lds[L3 + k], q, tc.mu, tc.nshift);
+        } else {
+            const ulonglong2* bp = reinterpret_cast<const ulonglong2*>(bdat + off + tid * 16);
+#pragma unroll
+            for (int k = 0; k < 8; k++) {
+                ulonglong2 bb = bp[k];
+                v[2 * k] = barrett_ref(v[2 * k], bb.x, q, tc.mu, tc.nshift);
+                v[2 * k + 1] = barrett_ref(v[2 * k + 1], bb.y, q, tc.mu, tc.nshift);
+            }
         }
         // no barrier: round 3' below rewrites only this thread's own LDS slots
     } else {
-        const ulonglong2* ip = reinterpret_cast<const ulonglong2*>(blk + tid * 16);
+        if (OFHE_COAL) {
 #pragma unroll
-        for (int k = 0; k < 8; k++) {
-            ulonglong2 a = ip[k];
-            v[2 * k] = a.x;
-            v[2 * k + 1] = a.y;
+            for (int k = 0; k < 16; k++) lds[L1 + 272 * k] = blk[tid + 256 * k];
+            __syncthreads();
+#pragma unroll
+            for (int k = 0; k < 16; k++) v[k] = lds[L3 + k];
+        } else {
+            const ulonglong2* ip = reinterpret_cast<const ulonglong2*>(blk + tid * 16);
+#pragma unroll
+            for (int k = 0; k < 8; k++) {
+                ulonglong2 a = ip[k];
+                v[2 * k] = a.x;
+                v[2 * k + 1] = a.y;
+            }
         }
     }
     // inverse round 3': st = 1, GS stages t = 1, 2, 4, 8 (s = 3, 2, 1, 0)
-    {
+    if (OFHE_TW3) {
+        const u64* itw3 = P.itw3 + (u64)t * (N / 16) * 30;
+        const u32 U = N >> 4, u = g * 256 + tid;
+        inv_stage16_t3<3>(v, itw3, U, u, tc, M);
+        inv_stage16_t3<2>(v, itw3, U, u, tc, M);
+        inv_stage16_t3<1>(v, itw3, U, u, tc, M);
+        inv_stage16_t3<0>(v, itw3, U, u, tc, M);
+    } else {
         const u32 M0 = (N >> 4) + g * 256 + tid;
         inv_stage16_first(v, itwn, (M0 << 3) - (N >> 1), tc, M);
         inv_stage16<2>(v, itw, M0, M);

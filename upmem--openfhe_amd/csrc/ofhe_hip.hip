@@ -163,6 +163,11 @@ int ofhe_hip_plan_create(ofhe_ctx_t ctx, uint32_t log_n, uint32_t towers, const 
     p->ninv.resize(towers);
     std::vector<TowerConst> tc(towers);
     std::vector<u64> tw(2 * TN), itw(2 * TN), itwn(TN);
+    // round-3 transposed tables (k_block, see ntt_kernels.hpp): per tower
+    // 15 U pairs, U = N/16, entry (S, j, u) at (2^S - 1) U + j U + u
+    const u32 U3 = N >= 4096 ? N / 16 : 0;
+    const size_t W3 = (size_t)15 * U3 * 2;  // words per tower
+    std::vector<u64> tw3(W3 * towers), itw3(W3 * towers);
     // PreCompute (transformnat-impl.h:708-763), one host thread per tower group
     auto build = [&](u32 t) {
         const u64 qt = q[t], ps = psi[t], psinv = invmod(ps, qt);
@@ -192,6 +197,22 @@ int ofhe_hip_plan_create(ofhe_ctx_t ctx, uint32_t log_n, uint32_t towers, const 
             itwn[(size_t)t * N + 2 * i] = w;
             itwn[(size_t)t * N + 2 * i + 1] = shoup_pre(w, qt);
         }
+        for (u32 S = 0; S < 4 && U3; S++)
+            for (u32 j = 0; j < (1u << S); j++)
+                for (u32 u = 0; u < U3; u++) {
+                    const size_t e = (size_t)t * W3 + 2 * ((size_t)((1u << S) - 1) * U3 + (size_t)j * U3 + u);
+                    const u32 idx = ((U3 + u) << S) + j;
+                    tw3[e] = T[idx];
+                    tw3[e + 1] = p->tab_pre[(size_t)t * N + idx];
+                    if (S == 3) {  // first inverse stage, N^-1 folded (itwn)
+                        const size_t i = idx - N / 2;
+                        itw3[e] = itwn[(size_t)t * N + 2 * i];
+                        itw3[e + 1] = itwn[(size_t)t * N + 2 * i + 1];
+                    } else {
+                        itw3[e] = TI[idx];
+                        itw3[e + 1] = p->itab_pre[(size_t)t * N + idx];
+                    }
+                }
         TowerConst c{};
         c.q = qt;
         c.ninv = ni;
@@ -226,6 +247,12 @@ int ofhe_hip_plan_create(ofhe_ctx_t ctx, uint32_t log_n, uint32_t towers, const 
     if (e == hipSuccess) e = hipMalloc(&p->d_tw, sizeof(u64) * 2 * TN);
     if (e == hipSuccess) e = hipMalloc(&p->d_itw, sizeof(u64) * 2 * TN);
     if (e == hipSuccess) e = hipMalloc(&p->d_itwn, sizeof(u64) * TN);
+    if (e == hipSuccess) e = hipMalloc(&p->d_tw3, sizeof(u64) * (tw3.size() ? tw3.size() : 2));
+    if (e == hipSuccess) e = hipMalloc(&p->d_itw3, sizeof(u64) * (itw3.size() ? itw3.size() : 2));
+    if (e == hipSuccess && tw3.size())
+        e = hipMemcpy(p->d_tw3, tw3.data(), sizeof(u64) * tw3.size(), hipMemcpyHostToDevice);
+    if (e == hipSuccess && itw3.size())
+        e = hipMemcpy(p->d_itw3, itw3.data(), sizeof(u64) * itw3.size(), hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMalloc(&p->d_scal, sizeof(u64) * 2 * towers);
     if (e == hipSuccess) e = hipMemcpy(p->d_tc, tc.data(), sizeof(TowerConst) * towers, hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMemcpy(p->d_tw, tw.data(), sizeof(u64) * 2 * TN, hipMemcpyHostToDevice);
@@ -268,6 +295,8 @@ int ofhe_hip_plan_destroy(ofhe_plan_t p) {
     (void)hipFree(p->d_tw);
     (void)hipFree(p->d_itw);
     (void)hipFree(p->d_itwn);
+    (void)hipFree(p->d_tw3);
+    (void)hipFree(p->d_itw3);
     (void)hipFree(p->d_scal);
     delete p;
     return OFHE_OK;
@@ -298,6 +327,8 @@ static PlanArgs args_of(ofhe_plan_t p, u32 t0 = 0, u32 count = 0) {
     a.tw = p->d_tw + 2 * N * t0;
     a.itw = p->d_itw + 2 * N * t0;
     a.itwn = p->d_itwn + N * t0;
+    a.tw3 = p->d_tw3 + (N >= 4096 ? (N / 16) * 30 * t0 : 0);
+    a.itw3 = p->d_itw3 + (N >= 4096 ? (N / 16) * 30 * t0 : 0);
     a.sstride = a.dstride = N * count;
     a.log_n = p->log_n;
     a.towers = count;
