@@ -71,9 +71,16 @@ __device__ __forceinline__ u32 xcd_remap(u32 bid, u32 nwg) {
 struct Tw {
     u64 w, wp;
 };
+// OFHE_ABL_NOTW (ablation builds only, wrong results): twiddles from
+// registers instead of memory, to measure what the loads cost.
 __device__ __forceinline__ Tw ldtw(const u64* base, u32 idx) {
+#ifdef OFHE_ABL_NOTW
+    const u64 f = (u64)(uintptr_t)base ^ idx;
+    return Tw{f & 0x0fffffffffffffffull, f * 0x9E3779B97F4A7C15ull};
+#else
     const ulonglong2 v = *reinterpret_cast<const ulonglong2*>(base + 2 * (u64)idx);
     return Tw{v.x, v.y};
+#endif
 }
 
 // Cooley-Tukey butterfly.  Two lazy-reduction schemes (OFHE_LAZY_FWD):
@@ -204,15 +211,13 @@ __device__ __forceinline__ void inv_round16(u64 (&v)[16], const u64* itw, u32 M0
 #endif
 // k_block's round-3 layout gives each thread 16 consecutive words, so direct
 // global access is one 128-byte line per lane per instruction.  With
-// OFHE_COAL the block's Hadamard operand, inverse input and forward output go
-// through LDS in the coalesced round-1 layout instead.
+// OFHE_COAL (inverse input, forward output) and OFHE_COAL_B (the Hadamard
+// operand) these go through the wave's own LDS slots instead (wave_stage_*).
 #ifndef OFHE_COAL
 #define OFHE_COAL 1
 #endif
-// Staging the Hadamard operand the same way costs two more barriers in the
-// fused kernel and measured 6 % slower there, so it is off.
 #ifndef OFHE_COAL_B
-#define OFHE_COAL_B 0
+#define OFHE_COAL_B 1
 #endif
 template <int S, class M_>
 __device__ __forceinline__ void fwd_stage16_t3(u64 (&v)[16], const u64* tw3, u32 U, u32 u, const M_& M) {
@@ -249,6 +254,42 @@ __device__ __forceinline__ void inv_stage16_t3(u64 (&v)[16], const u64* itw3, u3
 // and 2-way on one half-wave for round 1 (tools/lds_banks.py).
 __device__ __forceinline__ u32 lds_pad(u32 p) { return p + (p >> 4); }
 constexpr u32 LDS_WORDS = 4096 + 4096 / 16;
+
+// Wave-private staging through the round-3 LDS slots.  In round 3 thread t
+// owns block elements 16t + k at lds_pad = 17t + k, so wave w's 64 threads own
+// the 1024 consecutive elements [1024w, 1024w + 1024).  From a thread's
+// round-3 LDS reads until the next block barrier no other wave touches that
+// region, so a wave can turn its lane-strided (128 B per lane) global accesses
+// into contiguous ones through it without a block barrier: instruction k,
+// lane i moves elements 128k + 2i and 128k + 2i + 1 of the wave's range.
+// LDS processes one wave's operations in order; wave_barrier keeps the
+// compiler from reordering them across lanes.
+__device__ __forceinline__ void wave_stage_in(const u64* wsrc, u64* lds, u32 tid, u64 (&out)[16]) {
+    const u32 lane = tid & 63, base = (tid >> 6) * 1024;
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+        const ulonglong2 v = *reinterpret_cast<const ulonglong2*>(wsrc + 128 * k + 2 * lane);
+        const u32 p = base + 128 * k + 2 * lane;  // even: p, p + 1 share a 16-group
+        lds[lds_pad(p)] = v.x;
+        lds[lds_pad(p) + 1] = v.y;
+    }
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int k = 0; k < 16; k++) out[k] = lds[tid * 17 + k];
+    __builtin_amdgcn_wave_barrier();
+}
+__device__ __forceinline__ void wave_stage_out(const u64 (&v)[16], u64* lds, u32 tid, u64* wdst) {
+    const u32 lane = tid & 63, base = (tid >> 6) * 1024;
+#pragma unroll
+    for (int k = 0; k < 16; k++) lds[tid * 17 + k] = v[k];
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+        const u32 p = base + 128 * k + 2 * lane;
+        *reinterpret_cast<ulonglong2*>(wdst + 128 * k + 2 * lane) =
+            make_ulonglong2(lds[lds_pad(p)], lds[lds_pad(p) + 1]);
+    }
+}
 
 // ---------------------------------------------------------------------------
 // k_block: the last 12 stages on a 4096-element block; MODE selects
@@ -325,12 +366,7 @@ __global__ __launch_bounds__(256, OFHE_KB_WAVES) void k_block(PlanArgs P, const 
         for (int k = 0; k < 16; k++) v[k] = canon_fwd(v[k], q);
         if (MODE == MODE_FWD) {
             if (OFHE_COAL) {
-                // own L3 slots were this thread's round-3 inputs: no hazard
-#pragma unroll
-                for (int k = 0; k < 16; k++) lds[L3 + k] = v[k];
-                __syncthreads();
-#pragma unroll
-                for (int k = 0; k < 16; k++) oblk[tid + 256 * k] = lds[L1 + 272 * k];
+                wave_stage_out(v, lds, tid, oblk + (tid >> 6) * 1024);
             } else {
                 ulonglong2* o = reinterpret_cast<ulonglong2*>(oblk + tid * 16);
 #pragma unroll
@@ -340,18 +376,19 @@ __global__ __launch_bounds__(256, OFHE_KB_WAVES) void k_block(PlanArgs P, const 
         }
         // Hadamard with b (evaluation form), NativeVectorT::ModMulNoCheckEq
         if (OFHE_COAL_B) {
-            // b staged through LDS: coalesced rows in, this thread's 16 out
-            __syncthreads();  // every thread has read its round-3 inputs
+            u64 bb[16];
+            wave_stage_in(bdat + off + (tid >> 6) * 1024, lds, tid, bb);
 #pragma unroll
-            for (int k = 0; k < 16; k++) lds[L1 + 272 * k] = bdat[off + tid + 256 * k];
-            __syncthreads();
-#pragma unroll
-            for (int k = 0; k < 16; k++) v[k] = barrett_ref(v[k], lds[L3 + k], q, tc.mu, tc.nshift);
+            for (int k = 0; k < 16; k++) v[k] = barrett_ref(v[k], bb[k], q, tc.mu, tc.nshift);
         } else {
             const ulonglong2* bp = reinterpret_cast<const ulonglong2*>(bdat + off + tid * 16);
 #pragma unroll
             for (int k = 0; k < 8; k++) {
+#ifdef OFHE_ABL_NOB
+                ulonglong2 bb = make_ulonglong2(v[k] ^ off, v[k + 8] ^ tid);
+#else
                 ulonglong2 bb = bp[k];
+#endif
                 v[2 * k] = barrett_ref(v[2 * k], bb.x, q, tc.mu, tc.nshift);
                 v[2 * k + 1] = barrett_ref(v[2 * k + 1], bb.y, q, tc.mu, tc.nshift);
             }
@@ -359,11 +396,7 @@ __global__ __launch_bounds__(256, OFHE_KB_WAVES) void k_block(PlanArgs P, const 
         // no barrier: round 3' below rewrites only this thread's own LDS slots
     } else {
         if (OFHE_COAL) {
-#pragma unroll
-            for (int k = 0; k < 16; k++) lds[L1 + 272 * k] = blk[tid + 256 * k];
-            __syncthreads();
-#pragma unroll
-            for (int k = 0; k < 16; k++) v[k] = lds[L3 + k];
+            wave_stage_in(blk + (tid >> 6) * 1024, lds, tid, v);
         } else {
             const ulonglong2* ip = reinterpret_cast<const ulonglong2*>(blk + tid * 16);
 #pragma unroll
