@@ -79,6 +79,7 @@ struct Mod {
     u64 q8;   // 8q
     u64 nq;   // 2^64 - q   (loaded, not derived, so LLVM keeps the adds)
     u64 nq4;  // 2^64 - 4q
+    u64 nq8;  // 2^64 - 8q
     u32 sh;   // L - 32 (SPQ only)
 };
 
@@ -101,7 +102,7 @@ __device__ __forceinline__ u64 shoup_lazy(u64 a, u64 w, u64 wp, const Mod<SPQ>& 
 
 // canonical Shoup: ModMulFastConstEq semantics (result in [0, q)), generic q.
 __device__ __forceinline__ u64 shoup_canon(u64 a, u64 w, u64 wp, u64 q) {
-    const Mod<false> M{q, 4 * q, 8 * q, 0 - q, 0 - 4 * q, 0};
+    const Mod<false> M{q, 4 * q, 8 * q, 0 - q, 0 - 4 * q, 0 - 8 * q, 0};
     u64 r = shoup_lazy(a, w, wp, M);
     r = csub(r, 2 * q);
     return csub(r, q);

@@ -41,7 +41,7 @@ struct TowerConst {
 };
 template <bool SPQ>
 __device__ __forceinline__ Mod<SPQ> load_mod(const TowerConst& tc) {
-    return Mod<SPQ>{tc.q, 4 * tc.q, 8 * tc.q, tc.nq, tc.nq4, tc.spq_sh};
+    return Mod<SPQ>{tc.q, 4 * tc.q, 8 * tc.q, tc.nq, tc.nq4, 0 - 8 * tc.q, tc.spq_sh};
 }
 
 // Device view of a plan. Twiddles are interleaved (w, w') pairs so one
@@ -94,10 +94,29 @@ __device__ __forceinline__ Tw ldtw(const u64* base, u32 idx) {
 #ifndef OFHE_LAZY_FWD
 #define OFHE_LAZY_FWD 1
 #endif
-template <class M_>
-__device__ __forceinline__ void ct_bfly_cs(u64& x, u64& y, Tw w, const M_& M, bool cs) {
+// OFHE_THR (special primes q = 2^L - d only): the CS stages subtract 8q when
+// bit L+3 of x is set instead of comparing with 8q: one bit-field extract and
+// two ANDs build the mask, one 64-bit add applies it -- no compare, no VCC,
+// no selects.  2^(L+3) > 8q, so the invariant becomes [0, 2^(L+3) + 8q)
+// (< 2^(L+4) <= 2^64, where the bit test is exact); canon_fwd takes one more
+// conditional subtract.  Measured 3 % slower in the block pass despite the
+// shorter instruction stream (tools/exp_variants.py), so it is off.
+#ifndef OFHE_THR
+#define OFHE_THR 0
+#endif
+template <bool SPQ>
+__device__ __forceinline__ u64 csub_thr8(u64 x, const Mod<SPQ>& M) {
+    const u32 m = (u32)__builtin_amdgcn_sbfe((int)hi32(x), M.sh + 3, 1);
+    return x + pack(m & lo32(M.nq8), m & hi32(M.nq8));
+}
+template <bool SPQ>
+__device__ __forceinline__ void ct_bfly_cs(u64& x, u64& y, Tw w, const Mod<SPQ>& M, bool cs) {
     const u64 t = shoup_lazy(y, w.w, w.wp, M);  // [0, 4q)
-    const u64 a = OFHE_LAZY_FWD ? (cs ? csub(x, M.q8) : x) : csub(x, M.q4);
+    u64 a;
+    if (OFHE_LAZY_FWD)
+        a = cs ? ((SPQ && OFHE_THR) ? csub_thr8(x, M) : csub(x, M.q8)) : x;
+    else
+        a = csub(x, M.q4);
     x = a + t;
     y = a + M.q4 - t;
 }
@@ -130,8 +149,10 @@ __device__ __forceinline__ u64 canon8(u64 x, u64 q) {  // [0, 8q) -> [0, q)
     return csub(x, q);
 }
 // forward-transform output (any stage pattern) -> [0, q)
+template <bool SPQ>
 __device__ __forceinline__ u64 canon_fwd(u64 x, u64 q) {
-    if (OFHE_LAZY_FWD) x = csub(x, 8 * q);  // [0, 16q) -> [0, 8q)
+    if (SPQ && OFHE_THR) x = csub(x, 8 * q);  // [0, 2^(L+3) + 8q) -> [0, 8q + 8d)
+    if (OFHE_LAZY_FWD) x = csub(x, 8 * q);    // [0, 16q) -> [0, 8q)
     return canon8(x, q);
 }
 __device__ __forceinline__ u64 canon4(u64 x, u64 q) {  // [0, 4q) -> [0, q)
@@ -363,7 +384,7 @@ __global__ __launch_bounds__(256, OFHE_KB_WAVES) void k_block(PlanArgs P, const 
             fwd_round16(v, tw, (N >> 4) + g * 256 + tid, M);
         }
 #pragma unroll
-        for (int k = 0; k < 16; k++) v[k] = canon_fwd(v[k], q);
+        for (int k = 0; k < 16; k++) v[k] = canon_fwd<SPQ>(v[k], q);
         if (MODE == MODE_FWD) {
             if (OFHE_COAL) {
                 wave_stage_out(v, lds, tid, oblk + (tid >> 6) * 1024);
@@ -624,7 +645,7 @@ __global__ __launch_bounds__(256) void k_small(PlanArgs P, const u64* src, u64* 
             __syncthreads();
         }
         for (u32 i = threadIdx.x; i < N; i += blockDim.x) {
-            u64 x = canon_fwd(lds[i], q);
+            u64 x = canon_fwd<SPQ>(lds[i], q);
             if (MODE == MODE_FUSED) x = barrett_ref(x, bdat[off + i], q, tc.mu, tc.nshift);
             lds[i] = x;
         }
