@@ -204,6 +204,17 @@ def main():
         except Exception:
             traffic = None
 
+    # VALU issue rate of the dominant kernel from the SQ counters
+    # (tools/pmc_valu.sh -> profiles/pmc_valu.json): the path is bound by
+    # integer-VALU issue, not HBM
+    valu = None
+    vpath = os.path.join(ROOT, "profiles", "pmc_valu.json")
+    if os.path.exists(vpath):
+        try:
+            valu = json.load(open(vpath)).get("kernels", {}).get(dominant)
+        except Exception:
+            valu = None
+
     # spot parity check against the oracle (one tower of two batch entries)
     parity = None
     if not args.no_check and rank == 0:
@@ -266,7 +277,8 @@ def main():
                        "parallelism": f"batch-sharded x{world} (no data-path collective)"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": dominant,
-                         "kernel_ms": kms, "alg_bytes_per_launch": ALG_BYTES_PER_COEFF * coeffs_rank},
+                         "kernel_ms": kms, "alg_bytes_per_launch": ALG_BYTES_PER_COEFF * coeffs_rank,
+                         "valu_issue": valu},
             "pipeline_hbm_frac": value / world * ALG_BYTES_PER_COEFF / (HBM_PEAK_GBS * 1e9),
             "kernels_ms": kernels,
             "cpu_baseline": cpu,

@@ -17,7 +17,13 @@ def kind(nm):
     return None
 
 
+import json
+
 d = sys.argv[1]
+report = {"source": "rocprofv3 --pmc SQ_* GRBM_GUI_ACTIVE on tools/run_pipeline.py (N=2^16, 16 towers, batch 256)",
+          "note": "valu_inst_per_simd_cycle: SQ_INSTS_VALU / (1024 SIMDs x clock x time); a 4-cycle "
+                  "wave64 instruction stream saturates a SIMD at 0.25", "kernels": {}}
+names = {"block": "k_block<fused>", "cols_f": "colpass<fwd>", "cols_i": "colpass<inv>"}
 for vdir in sorted(glob.glob(os.path.join(d, "v*"))):
     if not os.path.isdir(vdir):
         continue
@@ -46,7 +52,17 @@ for vdir in sorted(glob.glob(os.path.join(d, "v*"))):
         if "GRBM_GUI_ACTIVE" in med and t:
             clk = med["GRBM_GUI_ACTIVE"] / 8 / t
             line = f"     clock={clk / 1e9:.2f} GHz"
+            ent = {"clock_ghz": round(clk / 1e9, 3), "kernel_ms": round(t * 1e3, 4)}
             if "SQ_INSTS_VALU" in med:
                 # VALU wave-instructions per SIMD per cycle (1024 SIMDs)
-                line += f" valu_inst/SIMD/cycle={med['SQ_INSTS_VALU'] / (1024 * clk * t):.3f}"
+                ipc = med["SQ_INSTS_VALU"] / (1024 * clk * t)
+                line += f" valu_inst/SIMD/cycle={ipc:.3f}"
+                ent["valu_inst_per_simd_cycle"] = round(ipc, 4)
+            if wc:
+                for c in ("SQ_ACTIVE_INST_VALU", "SQ_WAIT_INST_ANY", "SQ_WAIT_ANY"):
+                    if c in med:
+                        ent[c[3:].lower() + "_per_wave_cycle"] = round(med[c] / wc, 4)
+            report["kernels"].setdefault(names[k], ent)
             print(line)
+with open(os.path.join(d, "pmc_valu.json"), "w") as f:
+    json.dump(report, f, indent=1)
