@@ -118,8 +118,13 @@ int mod_down_run(const ModDownArgs& A, const u64* x, u64 xstride, u64* out, u64 
     B.gap = 0;
     RCCHK(bconv_run(B, sp.w(), sq.w(), batch, s));
     if (A.t_q) RCCHK(scale_towers(A.t_q, sq.w(), sq.w(), qs, qs, batch, A.size_q, log_n, s));
+    // SetFormat(EVALUATION), then ans_i = (x_i - switched_i) * PInvModq_i
+    // (1165-1173): one transform whose block pass applies the subtraction and
+    // the scalar while the values are in registers
+    if (log_n >= 12)
+        return plan_ntt_fwd_sub(A.plan_q, A.q0, A.size_q, sq.w(), qs, x, xstride, out, ostride,
+                                reinterpret_cast<const u64*>(A.pinv), batch, s);
     RCCHK(plan_ntt_range(A.plan_q, false, A.q0, A.size_q, sq.w(), sq.w(), qs, qs, batch, s));
-    // ans_i = (x_i - switched_i) * PInvModq_i (1167-1173)
     return sub_scale(A.pinv, x, sq.w(), out, xstride, qs, ostride, batch, A.size_q, log_n, s);
 }
 

@@ -15,6 +15,7 @@ namespace ofhe {
 struct TowerScalar {
     u64 q, s, sp;
 };
+static_assert(sizeof(TowerScalar) == 24, "PlanArgs::scal reads TowerScalar as [towers][3] words");
 
 // (pair index) -> (batch entry, tower, coefficient) for `towers` towers of N
 struct PairIndex {

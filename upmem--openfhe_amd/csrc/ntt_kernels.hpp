@@ -55,11 +55,16 @@ struct PlanArgs {
     const u64* itw3;       // [T][15N/16][2] round-3 inverse twiddles (stage t = 1 with N^-1)
     u64 sstride;           // words between batch entries of src (towers * N when dense)
     u64 dstride;           // words between batch entries of dst (and of the Hadamard operand)
+    u64 bstride;           // words between batch entries of the second operand (bdat)
+    const u64* scal;       // MODE_FWD_SUB: [towers][3] = (q, s, s') per tower of the range
     u32 log_n;
     u32 towers;            // towers in this launch (a plan range starts at tc[0])
 };
 
-enum { MODE_FWD = 0, MODE_INV = 1, MODE_FUSED = 2 };
+// MODE_FWD_SUB: forward transform whose output is (x - NTT(y)) * s_t mod q,
+// the last step of ApproxModDown (dcrtpoly-impl.h:1167-1173) fused into the
+// block pass (x = bdat with batch stride bstride, (s, s') per tower in scal).
+enum { MODE_FWD = 0, MODE_INV = 1, MODE_FUSED = 2, MODE_FWD_SUB = 3 };
 
 // Bijective XCD-aware block remap (cdna_hip_programming.md T1): consecutive
 // work items land on the same XCD.
@@ -335,6 +340,7 @@ __global__ __launch_bounds__(256, OFHE_KB_WAVES) void k_block(PlanArgs P, const 
     const u32 t = pb / batch, b = pb % batch;
     const u64 inner = (u64)t * N + ((u64)g << 12);
     const u64 off = (u64)b * P.dstride + inner;
+    const u64 boff = (u64)b * P.bstride + inner;
     const u64* blk = src + (u64)b * P.sstride + inner;
     u64* oblk = dst + off;
     const TowerConst tc = P.tc[t];
@@ -350,7 +356,7 @@ __global__ __launch_bounds__(256, OFHE_KB_WAVES) void k_block(PlanArgs P, const 
     const u32 L3 = tid * 17;     // lds_pad(16 tid + k)       = L3 + k
     u64 v[16];
 
-    if (MODE == MODE_FWD || MODE == MODE_FUSED) {
+    if (MODE == MODE_FWD || MODE == MODE_FUSED || MODE == MODE_FWD_SUB) {
         if (NR == 3) {
             // round 1: st = 256, p = tid + 256k
 #pragma unroll
@@ -385,6 +391,18 @@ __global__ __launch_bounds__(256, OFHE_KB_WAVES) void k_block(PlanArgs P, const 
         }
 #pragma unroll
         for (int k = 0; k < 16; k++) v[k] = canon_fwd<SPQ>(v[k], q);
+        if (MODE == MODE_FWD_SUB) {
+            u64 xx[16];
+            wave_stage_in(bdat + boff + (tid >> 6) * 1024, lds, tid, xx);
+            const u64 sc = P.scal[3 * t + 1], scp = P.scal[3 * t + 2];
+#pragma unroll
+            for (int k = 0; k < 16; k++) {
+                const u64 d = xx[k] < v[k] ? xx[k] + q - v[k] : xx[k] - v[k];  // ModSubFastEq
+                v[k] = shoup_canon(d, sc, scp, q);
+            }
+            wave_stage_out(v, lds, tid, oblk + (tid >> 6) * 1024);
+            return;
+        }
         if (MODE == MODE_FWD) {
             if (OFHE_COAL) {
                 wave_stage_out(v, lds, tid, oblk + (tid >> 6) * 1024);
@@ -398,11 +416,11 @@ __global__ __launch_bounds__(256, OFHE_KB_WAVES) void k_block(PlanArgs P, const 
         // Hadamard with b (evaluation form), NativeVectorT::ModMulNoCheckEq
         if (OFHE_COAL_B) {
             u64 bb[16];
-            wave_stage_in(bdat + off + (tid >> 6) * 1024, lds, tid, bb);
+            wave_stage_in(bdat + boff + (tid >> 6) * 1024, lds, tid, bb);
 #pragma unroll
             for (int k = 0; k < 16; k++) v[k] = barrett_ref(v[k], bb[k], q, tc.mu, tc.nshift);
         } else {
-            const ulonglong2* bp = reinterpret_cast<const ulonglong2*>(bdat + off + tid * 16);
+            const ulonglong2* bp = reinterpret_cast<const ulonglong2*>(bdat + boff + tid * 16);
 #pragma unroll
             for (int k = 0; k < 8; k++) {
 #ifdef OFHE_ABL_NOB

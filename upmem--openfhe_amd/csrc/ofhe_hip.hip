@@ -329,7 +329,8 @@ static PlanArgs args_of(ofhe_plan_t p, u32 t0 = 0, u32 count = 0) {
     a.itwn = p->d_itwn + N * t0;
     a.tw3 = p->d_tw3 + (N >= 4096 ? (N / 16) * 30 * t0 : 0);
     a.itw3 = p->d_itw3 + (N >= 4096 ? (N / 16) * 30 * t0 : 0);
-    a.sstride = a.dstride = N * count;
+    a.sstride = a.dstride = a.bstride = N * count;
+    a.scal = nullptr;
     a.log_n = p->log_n;
     a.towers = count;
     return a;
@@ -462,6 +463,25 @@ int plan_ntt_range(ofhe_plan_t p, bool inverse, u32 t0, u32 count, const u64* sr
             if (p->log_n > 12) launch_colpass(ad, p->spq, p->split8, true, dst, dst, batch, s);
         }
     }
+    return post_launch();
+}
+
+int plan_ntt_fwd_sub(ofhe_plan_t p, u32 t0, u32 count, u64* y, u64 ystride, const u64* x, u64 xstride, u64* out,
+                     u64 ostride, const u64* scal, u32 batch, hipStream_t s) {
+    if (!p || !p->ctx) return fail(OFHE_ERR_STATE, "plan is NULL or destroyed");
+    if (p->log_n < 12) return fail(OFHE_ERR_ARG, "fused forward + subtract needs log_n >= 12");
+    if (count == 0 || batch == 0) return OFHE_OK;
+    if (t0 + count > p->towers) return fail(OFHE_ERR_ARG, "tower range outside the plan");
+    HIPCHK(hipSetDevice(p->ctx->device));
+    PlanArgs a = args_of(p, t0, count);
+    a.sstride = a.dstride = ystride;
+    if (p->log_n > 12) launch_colpass(a, p->spq, p->split8, false, y, y, batch, s);
+    PlanArgs ab = a;
+    ab.sstride = ystride;
+    ab.dstride = ostride;
+    ab.bstride = xstride;
+    ab.scal = scal;
+    launch_block<MODE_FWD_SUB>(ab, p->spq, y, out, x, batch, s, p->split8);
     return post_launch();
 }
 }  // namespace ofhe
