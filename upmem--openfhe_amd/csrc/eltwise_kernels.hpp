@@ -137,6 +137,9 @@ __device__ __forceinline__ void limbs_to_u128(u64 a0, u64 a1, u64 a2, u64 a3, u6
 template <int PT>
 __global__ __launch_bounds__(256) void k_bconv_limb(BconvArgs A, const u64* __restrict__ x, u64* __restrict__ out,
                                                     u32 batch) {
+    // y limbs of every source tower, computed once per coefficient and kept
+    // in this thread's own LDS column across the P tiles (no barrier needed)
+    __shared__ u64 ys[BCONV_LIMB_QMAX][256];
     const u32 N = 1u << A.log_n;
     const u64 gid = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (gid >= (u64)batch * N) return;
@@ -144,13 +147,18 @@ __global__ __launch_bounds__(256) void k_bconv_limb(BconvArgs A, const u64* __re
     const u64* xb = x + (u64)b * A.in_stride + ri;
     u64* ob = out + (u64)b * A.out_stride + ri;
     const u32 ppad = (A.size_p + PT - 1) / PT * PT;
+    const u32 tid = threadIdx.x;
+    for (u32 i = 0; i < A.size_q; i++) {
+        const u64 y = shoup_canon(xb[(u64)i * N], A.qhinv[2 * i], A.qhinv[2 * i + 1], A.qv[i]);
+        ys[i][tid] = (y & LIMB_MASK) | ((y >> LIMB) << 32);
+    }
     for (u32 j0 = 0; j0 < A.size_p; j0 += PT) {
         u64 a0[PT], a1[PT], a2[PT], a3[PT];
 #pragma unroll
         for (int j = 0; j < PT; j++) a0[j] = a1[j] = a2[j] = a3[j] = 0;
         for (u32 i = 0; i < A.size_q; i++) {
-            const u64 y = shoup_canon(xb[(u64)i * N], A.qhinv[2 * i], A.qhinv[2 * i + 1], A.qv[i]);
-            const u32 y0 = (u32)(y & LIMB_MASK), y1 = (u32)(y >> LIMB);
+            const u64 yy = ys[i][tid];
+            const u32 y0 = lo32(yy), y1 = hi32(yy);
             const u64* cl = A.qhlimb + (u64)i * ppad + j0;
 #pragma unroll
             for (int j = 0; j < PT; j++) {

@@ -647,7 +647,8 @@ int ofhe_hip_bconv_create(ofhe_ctx_t ctx, uint32_t log_n, uint32_t size_q, uint3
         if (p[j] < 2 || p[j] >= (1ull << 60)) return fail(OFHE_ERR_ARG, "p out of range");
     // layout: qv[Q] | qhinv[2Q] | qhmodp[Q*P] | pv[P] | pmu[2P] | qhlimb[Q*Ppad]
     const u32 ppad = (size_p + BCONV_PT - 1) / BCONV_PT * BCONV_PT;
-    const size_t words = size_q + 2 * size_q + (size_t)size_q * size_p + size_p + 2 * size_p + (size_t)size_q * ppad;
+    const u32 qrows = size_q;
+    const size_t words = size_q + 2 * size_q + (size_t)size_q * size_p + size_p + 2 * size_p + (size_t)qrows * ppad;
     std::vector<u64> h(words);
     u64* qv = h.data();
     u64* qhinv = qv + size_q;
