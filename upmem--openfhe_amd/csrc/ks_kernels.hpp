@@ -141,6 +141,10 @@ __global__ __launch_bounds__(256) void k_ks_inner_bs(const KsTower* __restrict__
 #pragma unroll
         for (int k = 0; k < 4; k++) kl[j][k] = on ? ((w[k] & LIMB_MASK) | ((w[k] >> LIMB) << 32)) : 0;
     }
+#ifndef OFHE_KS_UNROLL
+#define OFHE_KS_UNROLL 1
+#endif
+#pragma unroll OFHE_KS_UNROLL
     for (u32 b = 0; b < batch; b++) {
         const u64* d = digits + (u64)b * beta * poly + inner;
         u64 acc[4][4];
