@@ -270,6 +270,11 @@ int main() {
         EXPECT_EQ(U.GetFormat() == Format::EVALUATION, true, "ModUp output format");
         DCRTPolyHip Y = ApproxModDown(U.Times(pmod), PQ, PP, *down, pinv);
         EXPECT_EQ(Y, X, "ModDown(P * ModUp(x))");
+        DCRTPolyHip PU = U.Times(pmod);
+        DCRTPolyHip Yn = ApproxModDown(PU, PQ, PP, *down, pinv, 65537);
+        EXPECT_EQ(Yn, X, "same with BGV t (named operand)");
+        DCRTPolyHip Y3 = ApproxModDown(U.Times(pmod), PQ, PP, *down, pinv, 3);
+        EXPECT_EQ(Y3, X, "same with BGV t = 3");
         DCRTPolyHip Yb = ApproxModDown(U.Times(pmod), PQ, PP, *down, pinv, 65537);  // temporary operand
         EXPECT_EQ(Yb, X, "same with BGV t");
         if (!(Yb == X)) {
@@ -365,7 +370,16 @@ int main() {
         for (Format f : {Format::EVALUATION, Format::COEFFICIENT}) {
             DCRTPolyHip X(P, f);
             X.SetValues(v, f);
-            EXPECT_EQ(X.AutomorphismTransform(k).AutomorphismTransform(kinv), X, "sigma_kinv(sigma_k(x))");
+            DCRTPolyHip Y = X.AutomorphismTransform(k).AutomorphismTransform(kinv);
+            EXPECT_EQ(Y, X, "sigma_kinv(sigma_k(x))");
+            if (!(Y == X)) {
+                auto a = Y.GetValues(), b = X.GetValues();
+                size_t bad = 0, first = a.size();
+                for (size_t i = 0; i < a.size(); i++)
+                    if (a[i] != b[i]) bad++, first = std::min(first, i);
+                std::printf("  format %d: %zu/%zu differ, first at %zu: %llu vs %llu\n", (int)f, bad, a.size(), first,
+                            (unsigned long long)a[first], (unsigned long long)b[first]);
+            }
         }
         DCRTPolyHip X(P, Format::EVALUATION);
         EXPECT_THROW(X.AutomorphismTransform(4), math_error, "even index");

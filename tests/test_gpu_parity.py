@@ -326,3 +326,23 @@ def test_special_prime_switch_identical(hip, O, monkeypatch):
         outs.append(host(xc))
     assert np.array_equal(outs[0], outs[1])
     assert np.array_equal(outs[0], O.ntt_mul_intt(a, b, O.Tables(n, qs, rs)))
+
+
+def test_stream_ordered_alloc_and_zero(hip):
+    """ofhe_hip_alloc_async / free_async / zero on a caller stream."""
+    import torch
+
+    H, ctx = hip
+    s = torch.cuda.Stream()
+    n = 1 << 20
+    with torch.cuda.stream(s):
+        p = ctx.alloc_async(n * 8, s.cuda_stream)
+        src = torch.arange(n, dtype=torch.int64, device="cuda")
+        ctx.copy_device(p, src.data_ptr(), n * 8, s.cuda_stream)
+        ctx.zero(p, n * 4, s.cuda_stream)  # first half
+        out = torch.empty(n, dtype=torch.int64, device="cuda")
+        ctx.copy_device(out.data_ptr(), p, n * 8, s.cuda_stream)
+        ctx.free_async(p, s.cuda_stream)
+    s.synchronize()
+    h = out.cpu().numpy()
+    assert not h[: n // 2].any() and np.array_equal(h[n // 2:], np.arange(n // 2, n))

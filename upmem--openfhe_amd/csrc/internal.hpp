@@ -108,4 +108,8 @@ struct ofhe_bconv_s {
     ofhe_ctx_t ctx = nullptr;
     ofhe::BconvArgs args{};
     ofhe::u64* d_mem = nullptr;
+    // per-call constant tables of ofhe_hip_approx_mod_down (grow-only)
+    std::mutex tab_mu;
+    ofhe::u64* d_tab = nullptr;
+    size_t tab_words = 0;
 };

@@ -74,14 +74,6 @@ struct Scratch {
     }
 };
 
-// small constant table staged for one call (host memory must outlive the copy)
-int stage_table(Scratch& sc, const void* host, size_t bytes, hipStream_t s) {
-    RCCHK(sc.alloc(bytes, s));
-    HIPCHK(hipMemcpyAsync(sc.p, host, bytes, hipMemcpyHostToDevice, s));
-    HIPCHK(hipStreamSynchronize(s));
-    return OFHE_OK;
-}
-
 int copy_rows(u64* dst, u64 dstride, const u64* src, u64 sstride, u64 words, u32 rows, hipStream_t s) {
     if (!words || !rows) return OFHE_OK;
     HIPCHK(hipMemcpy2DAsync(dst, dstride * 8, src, sstride * 8, words * 8, rows, hipMemcpyDeviceToDevice, s));
@@ -177,12 +169,29 @@ int ofhe_hip_approx_mod_down(ofhe_plan_t pq, ofhe_plan_t pp, ofhe_bconv_t bc, co
         for (u32 j = 0; j < P; j++) tab[Q + j] = scalar_of(pp->q[j], invmod(t % pp->q[j], pp->q[j]));  // tInvModp
         for (u32 i = 0; i < Q; i++) tab[Q + P + i] = scalar_of(pq->q[i], t);                          // t mod q_i
     }
-    Scratch dt;
-    RCCHK(stage_table(dt, tab.data(), tab.size() * sizeof(TowerScalar), s));
-    const TowerScalar* d = (const TowerScalar*)dt.p;
+    // Constant tables live in the converter (grow-only) and are written with
+    // a blocking copy after draining the device: a copy from pageable memory
+    // into stream-ordered (pool) memory was observed to race with the
+    // kernels that read it.  The lock keeps concurrent callers of this
+    // converter from overwriting each other's tables.
+    std::lock_guard<std::mutex> lk(bc->tab_mu);
+    const size_t words = tab.size() * 3;
+    if (bc->tab_words < words) {
+        HIPCHK(hipDeviceSynchronize());
+        (void)hipFree(bc->d_tab);
+        bc->d_tab = nullptr;
+        bc->tab_words = 0;
+        HIPCHK(hipMalloc(&bc->d_tab, words * sizeof(u64)));
+        bc->tab_words = words;
+    }
+    HIPCHK(hipDeviceSynchronize());
+    HIPCHK(hipMemcpy(bc->d_tab, tab.data(), words * sizeof(u64), hipMemcpyHostToDevice));
+    const TowerScalar* d = (const TowerScalar*)bc->d_tab;
     ModDownArgs A{pq, pp, 0, 0, Q, P, bc->args, d, t ? d + Q : nullptr, t ? d + Q + P : nullptr};
     const u64 N = 1ull << pq->log_n;
-    return mod_down_run(A, x, (u64)(Q + P) * N, out, (u64)Q * N, batch, s);
+    RCCHK(mod_down_run(A, x, (u64)(Q + P) * N, out, (u64)Q * N, batch, s));
+    HIPCHK(hipStreamSynchronize(s));  // the tables stay in use until the kernels finish
+    return OFHE_OK;
 }
 
 // ---------------------------------------------------------------------------

@@ -625,9 +625,10 @@ int ofhe_hip_modmul_scalar(ofhe_plan_t p, const uint64_t* a, const uint64_t* s, 
     // the plan's mutex so concurrent callers on one plan do not race on it.
     std::lock_guard<std::mutex> lk(p->scal_mu);
     HIPCHK(hipSetDevice(p->ctx->device));
-    hipStream_t st = pick(stream);
-    HIPCHK(hipMemcpyAsync(p->d_scal, sp.data(), sizeof(u64) * sp.size(), hipMemcpyHostToDevice, st));
-    HIPCHK(hipStreamSynchronize(st));
+    // an earlier modmul_scalar (on any stream) may still read d_scal: drain
+    // the device, then a blocking copy
+    HIPCHK(hipDeviceSynchronize());
+    HIPCHK(hipMemcpy(p->d_scal, sp.data(), sizeof(u64) * sp.size(), hipMemcpyHostToDevice));
     return eltwise<ELT_MULS>(p, a, p->d_scal, c, batch, stream);
 }
 
@@ -706,6 +707,7 @@ int ofhe_hip_bconv_destroy(ofhe_bconv_t b) {
     if (!b) return fail(OFHE_ERR_ARG, "bconv is NULL");
     if (b->ctx) (void)hipSetDevice(b->ctx->device);
     (void)hipFree(b->d_mem);
+    (void)hipFree(b->d_tab);
     delete b;
     return OFHE_OK;
 }

@@ -59,15 +59,18 @@ public:
     }
     ofhe_ctx_t ctx() const { return ctx_; }
     int device() const { return device_; }
-    // Stream-ordered on the default stream every adapter op uses: a buffer
-    // dropped while kernels that read it are still queued stays valid until
-    // they finish (DCRTPoly temporaries die right after the call that uses them).
     void* allocate(size_t bytes) {
         void* p = nullptr;
-        check(ofhe_hip_alloc_async(ctx_, bytes, &p, nullptr), "HipManager::allocate");
+        check(ofhe_hip_alloc(ctx_, bytes, &p), "HipManager::allocate");
         return p;
     }
-    void deallocate(void* p) { check(ofhe_hip_free_async(ctx_, p, nullptr), "HipManager::deallocate"); }
+    // A buffer may be dropped while kernels that read it are still queued
+    // (DCRTPoly temporaries die right after the call that uses them): drain
+    // the stream every adapter op uses before releasing it.
+    void deallocate(void* p) {
+        sync();
+        check(ofhe_hip_free(ctx_, p), "HipManager::deallocate");
+    }
     void zero(void* dst, size_t bytes) { check(ofhe_hip_zero(ctx_, dst, bytes, nullptr), "HipManager::zero"); }
     // Host <-> device copies of pageable memory are bracketed by stream syncs:
     // HIP may stage them outside the stream's order, and the host buffer may
@@ -110,7 +113,10 @@ public:
         return *this;
     }
     ~DeviceBuffer() {
-        if (p_) ofhe_hip_free_async(m_->ctx(), p_, nullptr);
+        if (p_) {
+            (void)ofhe_hip_sync(m_->ctx(), nullptr);
+            (void)ofhe_hip_free(m_->ctx(), p_);
+        }
     }
     uint64_t* get() const { return p_; }
     size_t size() const { return n_; }
