@@ -76,6 +76,32 @@ __device__ __forceinline__ u32 xcd_remap(u32 bid, u32 nwg) {
 struct Tw {
     u64 w, wp;
 };
+
+// Streaming (non-temporal) access for polynomial data, so that the data
+// streaming through L2 does not evict the twiddles every block re-reads
+// (OFHE_NT, A/B switch).
+#ifndef OFHE_NT
+#define OFHE_NT 1
+#endif
+typedef u64 u64x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ u64 ld_s(const u64* p) { return OFHE_NT ? __builtin_nontemporal_load(p) : *p; }
+__device__ __forceinline__ void st_s(u64* p, u64 v) {
+    if (OFHE_NT)
+        __builtin_nontemporal_store(v, p);
+    else
+        *p = v;
+}
+__device__ __forceinline__ u64x2 ld2_s(const u64* p) {
+    const u64x2* q = reinterpret_cast<const u64x2*>(p);
+    return OFHE_NT ? __builtin_nontemporal_load(q) : *q;
+}
+__device__ __forceinline__ void st2_s(u64* p, u64x2 v) {
+    u64x2* q = reinterpret_cast<u64x2*>(p);
+    if (OFHE_NT)
+        __builtin_nontemporal_store(v, q);
+    else
+        *q = v;
+}
 // OFHE_ABL_NOTW (ablation builds only, wrong results): twiddles from
 // registers instead of memory, to measure what the loads cost.
 __device__ __forceinline__ Tw ldtw(const u64* base, u32 idx) {
@@ -294,7 +320,7 @@ __device__ __forceinline__ void wave_stage_in(const u64* wsrc, u64* lds, u32 tid
     const u32 lane = tid & 63, base = (tid >> 6) * 1024;
 #pragma unroll
     for (int k = 0; k < 8; k++) {
-        const ulonglong2 v = *reinterpret_cast<const ulonglong2*>(wsrc + 128 * k + 2 * lane);
+        const u64x2 v = ld2_s(wsrc + 128 * k + 2 * lane);
         const u32 p = base + 128 * k + 2 * lane;  // even: p, p + 1 share a 16-group
         lds[lds_pad(p)] = v.x;
         lds[lds_pad(p) + 1] = v.y;
@@ -312,8 +338,10 @@ __device__ __forceinline__ void wave_stage_out(const u64 (&v)[16], u64* lds, u32
 #pragma unroll
     for (int k = 0; k < 8; k++) {
         const u32 p = base + 128 * k + 2 * lane;
-        *reinterpret_cast<ulonglong2*>(wdst + 128 * k + 2 * lane) =
-            make_ulonglong2(lds[lds_pad(p)], lds[lds_pad(p) + 1]);
+        u64x2 w;
+        w.x = lds[lds_pad(p)];
+        w.y = lds[lds_pad(p) + 1];
+        st2_s(wdst + 128 * k + 2 * lane, w);
     }
 }
 
@@ -360,7 +388,7 @@ __global__ __launch_bounds__(256, OFHE_KB_WAVES) void k_block(PlanArgs P, const 
         if (NR == 3) {
             // round 1: st = 256, p = tid + 256k
 #pragma unroll
-            for (int k = 0; k < 16; k++) v[k] = blk[tid + 256 * k];
+            for (int k = 0; k < 16; k++) v[k] = ld_s(blk + tid + 256 * k);
             fwd_round16(v, tw, (N >> 12) + g, M);
 #pragma unroll
             for (int k = 0; k < 16; k++) lds[L1 + 272 * k] = v[k];
@@ -370,7 +398,7 @@ __global__ __launch_bounds__(256, OFHE_KB_WAVES) void k_block(PlanArgs P, const 
             for (int k = 0; k < 16; k++) v[k] = lds[L2 + 17 * k];
         } else {
 #pragma unroll
-            for (int k = 0; k < 16; k++) v[k] = blk[h * 256 + r + 16 * k];
+            for (int k = 0; k < 16; k++) v[k] = ld_s(blk + h * 256 + r + 16 * k);
         }
         fwd_round16(v, tw, (N >> 8) + g * 16 + h, M);
 #pragma unroll
@@ -469,7 +497,7 @@ __global__ __launch_bounds__(256, OFHE_KB_WAVES) void k_block(PlanArgs P, const 
     inv_round16(v, itw, (N >> 8) + g * 16 + h, M);
     if (NR == 2) {
 #pragma unroll
-        for (int k = 0; k < 16; k++) oblk[h * 256 + r + 16 * k] = v[k];
+        for (int k = 0; k < 16; k++) st_s(oblk + h * 256 + r + 16 * k, v[k]);
         return;
     }
 #pragma unroll
@@ -483,7 +511,7 @@ __global__ __launch_bounds__(256, OFHE_KB_WAVES) void k_block(PlanArgs P, const 
         for (int k = 0; k < 16; k++) v[k] = canon4(v[k], q);
     }
 #pragma unroll
-    for (int k = 0; k < 16; k++) oblk[tid + 256 * k] = v[k];
+    for (int k = 0; k < 16; k++) st_s(oblk + tid + 256 * k, v[k]);
 }
 
 // ---------------------------------------------------------------------------
@@ -520,7 +548,7 @@ __global__ __launch_bounds__(256, OFHE_KB_WAVES) void k_tcols(PlanArgs P, const 
         const u64* tw = P.tw + (u64)t * N * 2;
         // round 1: rows h + 16k (p = tid + 256k), stages m = 1..8
 #pragma unroll
-        for (int k = 0; k < 16; k++) v[k] = x[(u64)(h + 16 * k) * S + r];
+        for (int k = 0; k < 16; k++) v[k] = ld_s(x + (u64)(h + 16 * k) * S + r);
         fwd_round16(v, tw, 1, M);
 #pragma unroll
         for (int k = 0; k < 16; k++) lds[L1 + 272 * k] = v[k];
@@ -530,11 +558,11 @@ __global__ __launch_bounds__(256, OFHE_KB_WAVES) void k_tcols(PlanArgs P, const 
         for (int k = 0; k < 16; k++) v[k] = lds[L2 + 17 * k];
         fwd_round16(v, tw, 16 + h, M);
 #pragma unroll
-        for (int k = 0; k < 16; k++) y[(u64)(16 * h + k) * S + r] = v[k];
+        for (int k = 0; k < 16; k++) st_s(y + (u64)(16 * h + k) * S + r, v[k]);
     } else {
         const u64* itw = P.itw + (u64)t * N * 2;
 #pragma unroll
-        for (int k = 0; k < 16; k++) v[k] = x[(u64)(16 * h + k) * S + r];
+        for (int k = 0; k < 16; k++) v[k] = ld_s(x + (u64)(16 * h + k) * S + r);
         inv_round16(v, itw, 16 + h, M);
 #pragma unroll
         for (int k = 0; k < 16; k++) lds[L2 + 17 * k] = v[k];
@@ -543,7 +571,7 @@ __global__ __launch_bounds__(256, OFHE_KB_WAVES) void k_tcols(PlanArgs P, const 
         for (int k = 0; k < 16; k++) v[k] = lds[L1 + 272 * k];
         inv_round16(v, itw, 1, M);
 #pragma unroll
-        for (int k = 0; k < 16; k++) y[(u64)(h + 16 * k) * S + r] = canon4(v[k], q);
+        for (int k = 0; k < 16; k++) st_s(y + (u64)(h + 16 * k) * S + r, canon4(v[k], q));
     }
 }
 
