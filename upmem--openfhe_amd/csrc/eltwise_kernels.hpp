@@ -82,7 +82,7 @@ __global__ __launch_bounds__(256) void k_bconv(BconvArgs A, const u64* __restric
         for (int j = 0; j < PT; j++) lo[j] = hi[j] = 0;
         const u32 jn = min((u32)PT, A.size_p - j0);
         for (u32 i = 0; i < A.size_q; i++) {
-            const u64 y = shoup_canon(xb[(u64)i * N], A.qhinv[2 * i], A.qhinv[2 * i + 1], A.qv[i]);
+            const u64 y = shoup_canon(ld_s(xb + (u64)i * N), A.qhinv[2 * i], A.qhinv[2 * i + 1], A.qv[i]);
             const u64* qm = A.qhmodp + (u64)i * A.size_p + j0;
 #pragma unroll
             for (int j = 0; j < PT; j++) {
@@ -149,7 +149,7 @@ __global__ __launch_bounds__(256) void k_bconv_limb(BconvArgs A, const u64* __re
     const u32 ppad = (A.size_p + PT - 1) / PT * PT;
     const u32 tid = threadIdx.x;
     for (u32 i = 0; i < A.size_q; i++) {
-        const u64 y = shoup_canon(xb[(u64)i * N], A.qhinv[2 * i], A.qhinv[2 * i + 1], A.qv[i]);
+        const u64 y = shoup_canon(ld_s(xb + (u64)i * N), A.qhinv[2 * i], A.qhinv[2 * i + 1], A.qv[i]);
         ys[i][tid] = (y & LIMB_MASK) | ((y >> LIMB) << 32);
     }
     for (u32 j0 = 0; j0 < A.size_p; j0 += PT) {
@@ -176,7 +176,7 @@ __global__ __launch_bounds__(256) void k_bconv_limb(BconvArgs A, const u64* __re
                 u64 lo, hi;
                 limbs_to_u128(a0[j], a1[j], a2[j], a3[j], lo, hi);
                 const u32 jo = jj >= A.gap_at ? jj + A.gap : jj;
-                ob[(u64)jo * N] = barrett128(lo, hi, A.pv[jj], A.pmu[2 * jj], A.pmu[2 * jj + 1]);
+                st_s(ob + (u64)jo * N, barrett128(lo, hi, A.pv[jj], A.pmu[2 * jj], A.pmu[2 * jj + 1]));
             }
         }
     }

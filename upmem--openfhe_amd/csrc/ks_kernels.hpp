@@ -135,8 +135,8 @@ __global__ __launch_bounds__(256) void k_ks_inner_bs(const KsTower* __restrict__
     for (int j = 0; j < BMAX; j++) {
         const bool on = j < (int)beta;
         const u64 off = T.key_off + c + (u64)(on ? j : 0) * key_stride;
-        const ulonglong2 vb = *reinterpret_cast<const ulonglong2*>(kb + off);
-        const ulonglong2 va = *reinterpret_cast<const ulonglong2*>(ka + off);
+        const u64x2 vb = ld2_s(kb + off);
+        const u64x2 va = ld2_s(ka + off);
         const u64 w[4] = {vb.x, vb.y, va.x, va.y};
 #pragma unroll
         for (int k = 0; k < 4; k++) kl[j][k] = on ? ((w[k] & LIMB_MASK) | ((w[k] >> LIMB) << 32)) : 0;
@@ -152,7 +152,7 @@ __global__ __launch_bounds__(256) void k_ks_inner_bs(const KsTower* __restrict__
         for (int k = 0; k < 4; k++) acc[k][0] = acc[k][1] = acc[k][2] = acc[k][3] = 0;
 #pragma unroll
         for (int j = 0; j < BMAX; j++) {
-            const ulonglong2 x = *reinterpret_cast<const ulonglong2*>(d + (u64)(j < (int)beta ? j : 0) * poly);
+            const u64x2 x = ld2_s(d + (u64)(j < (int)beta ? j : 0) * poly);
             const u32 x0[2] = {(u32)(x.x & LIMB_MASK), (u32)(x.y & LIMB_MASK)};
             const u32 x1[2] = {(u32)(x.x >> LIMB), (u32)(x.y >> LIMB)};
 #pragma unroll
@@ -172,8 +172,13 @@ __global__ __launch_bounds__(256) void k_ks_inner_bs(const KsTower* __restrict__
             r[k] = barrett128(lo, hi, T.m, T.mu_lo, T.mu_hi);
         }
         const u64 o = (u64)b * poly + inner;
-        *reinterpret_cast<ulonglong2*>(ct0 + o) = make_ulonglong2(r[0], r[1]);
-        *reinterpret_cast<ulonglong2*>(ct1 + o) = make_ulonglong2(r[2], r[3]);
+        u64x2 w0, w1;
+        w0.x = r[0];
+        w0.y = r[1];
+        w1.x = r[2];
+        w1.y = r[3];
+        st2_s(ct0 + o, w0);
+        st2_s(ct1 + o, w1);
     }
 }
 

@@ -632,11 +632,11 @@ __global__ __launch_bounds__(256) void k_cols(PlanArgs P, const u64* src, u64* d
 #pragma unroll
     for (int k = 0; k < E; k++) {
         if (CPT == 2) {
-            const ulonglong2 p = *reinterpret_cast<const ulonglong2*>(x + (u64)k * 4096);
+            const u64x2 p = ld2_s(x + (u64)k * 4096);
             v[0][k] = p.x;
             v[CPT - 1][k] = p.y;
         } else {
-            v[0][k] = x[(u64)k * 4096];
+            v[0][k] = ld_s(x + (u64)k * 4096);
         }
     }
     if (!INV) {
@@ -650,10 +650,14 @@ __global__ __launch_bounds__(256) void k_cols(PlanArgs P, const u64* src, u64* d
     }
 #pragma unroll
     for (int k = 0; k < E; k++) {
-        if (CPT == 2)
-            *reinterpret_cast<ulonglong2*>(y + (u64)k * 4096) = make_ulonglong2(v[0][k], v[CPT - 1][k]);
-        else
-            y[(u64)k * 4096] = v[0][k];
+        if (CPT == 2) {
+            u64x2 w;
+            w.x = v[0][k];
+            w.y = v[CPT - 1][k];
+            st2_s(y + (u64)k * 4096, w);
+        } else {
+            st_s(y + (u64)k * 4096, v[0][k]);
+        }
     }
 }
 
