@@ -133,6 +133,22 @@ __device__ __forceinline__ u64 barrett_ref(u64 a, u64 b, u64 q, u64 mu, u32 n_sh
     return r >= q ? r - q : r;
 }
 
+// Montgomery product a*b*2^-64 mod q in [0, 2q) for a*b < q*2^64 (here
+// a < 16q lazy, b < q canonical, q < 2^60): t = a*b, m = -t*q^-1 mod 2^64,
+// u = (t + m*q) / 2^64 exactly.  qinv_neg = -q^-1 mod 2^64.
+__device__ __forceinline__ u64 mont_mul(u64 a, u64 b, u64 q, u64 qinv_neg) {
+    u64 tl, th;
+    {
+        u64 p00 = mad32(lo32(a), lo32(b), 0);
+        u64 m1 = mad32(lo32(a), hi32(b), (u64)hi32(p00));
+        u64 m2 = mad32(hi32(a), lo32(b), (u64)lo32(m1));
+        th = mad32(hi32(a), hi32(b), (u64)hi32(m1)) + (u64)hi32(m2);
+        tl = ((u64)lo32(m2) << 32) | lo32(p00);
+    }
+    const u64 m = tl * qinv_neg;
+    return th + mulhi_exact(m, q) + (tl != 0);
+}
+
 // Exact 64x64 -> 128 product (for base conversion accumulation).
 __device__ __forceinline__ void mul128(u64 a, u64 b, u64& lo, u64& hi) {
     u64 p00 = mad32(lo32(a), lo32(b), 0);

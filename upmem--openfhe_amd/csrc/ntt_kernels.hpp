@@ -38,6 +38,9 @@ struct TowerConst {
     u64 nq4;       // 2^64 - 4q   the lazy adds back into carry-chain subtractions)
     u32 nshift;    // msb(q) - 2
     u32 spq_sh;    // msb(q) - 32 when q = 2^msb - d with d < 2^32, else 0
+    u64 qinv_neg;  // -q^-1 mod 2^64 (Montgomery Hadamard)
+    u64 ninv_r;    // N^-1 * 2^64 mod q, and its Shoup precon: the fused
+    u64 ninv_r_pre;//   pipeline's first inverse stage undoes the 2^-64
 };
 template <bool SPQ>
 __device__ __forceinline__ Mod<SPQ> load_mod(const TowerConst& tc) {
@@ -53,6 +56,7 @@ struct PlanArgs {
     const u64* itwn;       // [T][N/2][2] TableI[N/2 + i] * N^-1 (first inverse stage)
     const u64* tw3;        // [T][15N/16][2] round-3 forward twiddles, lane-contiguous (log_n >= 12)
     const u64* itw3;       // [T][15N/16][2] round-3 inverse twiddles (stage t = 1 with N^-1)
+    const u64* itw3r;      // [T][N/2][2] the t = 1 section of itw3 times 2^64 mod q (fused, OFHE_MONT)
     u64 sstride;           // words between batch entries of src (towers * N when dense)
     u64 dstride;           // words between batch entries of dst (and of the Hadamard operand)
     u64 bstride;           // words between batch entries of the second operand (bdat)
@@ -261,6 +265,14 @@ __device__ __forceinline__ void inv_round16(u64 (&v)[16], const u64* itw, u32 M0
 #ifndef OFHE_TW3
 #define OFHE_TW3 1
 #endif
+// OFHE_MONT (needs OFHE_TW3): the fused pipeline's Hadamard is a Montgomery
+// product on the lazy forward output (no canonicalisation, no Barrett), and
+// the 2^-64 it introduces is cancelled by 2^64 folded into the first inverse
+// stage's N^-1 twiddles.  Intermediate values differ in representation only;
+// the canonical output is the same integer.
+#ifndef OFHE_MONT
+#define OFHE_MONT 1
+#endif
 // k_block's round-3 layout gives each thread 16 consecutive words, so direct
 // global access is one 128-byte line per lane per instruction.  With
 // OFHE_COAL (inverse input, forward output) and OFHE_COAL_B (the Hadamard
@@ -271,6 +283,7 @@ __device__ __forceinline__ void inv_round16(u64 (&v)[16], const u64* itw, u32 M0
 #ifndef OFHE_COAL_B
 #define OFHE_COAL_B 1
 #endif
+constexpr bool kMontFused = OFHE_MONT && OFHE_TW3 && OFHE_COAL_B;
 template <int S, class M_>
 __device__ __forceinline__ void fwd_stage16_t3(u64 (&v)[16], const u64* tw3, u32 U, u32 u, const M_& M) {
     constexpr int half = 8 >> S;
@@ -282,18 +295,18 @@ __device__ __forceinline__ void fwd_stage16_t3(u64 (&v)[16], const u64* tw3, u32
         for (int k = j * 2 * half; k < j * 2 * half + half; k++) ct_bfly<S & 1>(v[k], v[k + half], w, M);
     }
 }
+// base = this stage's section (itw3 + 2 (2^S - 1) U, or itw3r for S = 3)
 template <int S, class M_>
-__device__ __forceinline__ void inv_stage16_t3(u64 (&v)[16], const u64* itw3, u32 U, u32 u, const TowerConst& tc,
+__device__ __forceinline__ void inv_stage16_t3(u64 (&v)[16], const u64* base, u32 U, u32 u, u64 ninv, u64 ninv_pre,
                                                const M_& M) {
     constexpr int half = 8 >> S;
-    const u64* base = itw3 + 2 * (u64)(((1u << S) - 1) * U);
 #pragma unroll
     for (int j = 0; j < (1 << S); j++) {
         Tw w = ldtw(base + 2 * (u64)j * U, u);
 #pragma unroll
         for (int k = j * 2 * half; k < j * 2 * half + half; k++) {
             if (S == 3)
-                gs_bfly_ninv(v[k], v[k + half], w, tc.ninv, tc.ninv_pre, M);
+                gs_bfly_ninv(v[k], v[k + half], w, ninv, ninv_pre, M);
             else
                 gs_bfly(v[k], v[k + half], w, M);
         }
@@ -417,8 +430,10 @@ __global__ __launch_bounds__(256, OFHE_KB_WAVES) void k_block(PlanArgs P, const 
         } else {
             fwd_round16(v, tw, (N >> 4) + g * 256 + tid, M);
         }
+        if (!(MODE == MODE_FUSED && kMontFused)) {
 #pragma unroll
-        for (int k = 0; k < 16; k++) v[k] = canon_fwd<SPQ>(v[k], q);
+            for (int k = 0; k < 16; k++) v[k] = canon_fwd<SPQ>(v[k], q);
+        }
         if (MODE == MODE_FWD_SUB) {
             u64 xx[16];
             wave_stage_in(bdat + boff + (tid >> 6) * 1024, lds, tid, xx);
@@ -445,8 +460,13 @@ __global__ __launch_bounds__(256, OFHE_KB_WAVES) void k_block(PlanArgs P, const 
         if (OFHE_COAL_B) {
             u64 bb[16];
             wave_stage_in(bdat + boff + (tid >> 6) * 1024, lds, tid, bb);
+            if (kMontFused) {
 #pragma unroll
-            for (int k = 0; k < 16; k++) v[k] = barrett_ref(v[k], bb[k], q, tc.mu, tc.nshift);
+                for (int k = 0; k < 16; k++) v[k] = mont_mul(v[k], bb[k], q, tc.qinv_neg);  // [0, 2q)
+            } else {
+#pragma unroll
+                for (int k = 0; k < 16; k++) v[k] = barrett_ref(v[k], bb[k], q, tc.mu, tc.nshift);
+            }
         } else {
             const ulonglong2* bp = reinterpret_cast<const ulonglong2*>(bdat + boff + tid * 16);
 #pragma unroll
@@ -478,10 +498,13 @@ __global__ __launch_bounds__(256, OFHE_KB_WAVES) void k_block(PlanArgs P, const 
     if (OFHE_TW3) {
         const u64* itw3 = P.itw3 + (u64)t * (N / 16) * 30;
         const u32 U = N >> 4, u = g * 256 + tid;
-        inv_stage16_t3<3>(v, itw3, U, u, tc, M);
-        inv_stage16_t3<2>(v, itw3, U, u, tc, M);
-        inv_stage16_t3<1>(v, itw3, U, u, tc, M);
-        inv_stage16_t3<0>(v, itw3, U, u, tc, M);
+        if (MODE == MODE_FUSED && kMontFused)  // undo the Montgomery 2^-64 with the N^-1 fold
+            inv_stage16_t3<3>(v, P.itw3r + (u64)t * N, U, u, tc.ninv_r, tc.ninv_r_pre, M);
+        else
+            inv_stage16_t3<3>(v, itw3 + 2 * (u64)7 * U, U, u, tc.ninv, tc.ninv_pre, M);
+        inv_stage16_t3<2>(v, itw3 + 2 * (u64)3 * U, U, u, 0, 0, M);
+        inv_stage16_t3<1>(v, itw3 + 2 * (u64)1 * U, U, u, 0, 0, M);
+        inv_stage16_t3<0>(v, itw3, U, u, 0, 0, M);
     } else {
         const u32 M0 = (N >> 4) + g * 256 + tid;
         inv_stage16_first(v, itwn, (M0 << 3) - (N >> 1), tc, M);

@@ -167,7 +167,7 @@ int ofhe_hip_plan_create(ofhe_ctx_t ctx, uint32_t log_n, uint32_t towers, const 
     // 15 U pairs, U = N/16, entry (S, j, u) at (2^S - 1) U + j U + u
     const u32 U3 = N >= 4096 ? N / 16 : 0;
     const size_t W3 = (size_t)15 * U3 * 2;  // words per tower
-    std::vector<u64> tw3(W3 * towers), itw3(W3 * towers);
+    std::vector<u64> tw3(W3 * towers), itw3(W3 * towers), itw3r((size_t)(U3 ? N : 0) * towers);
     // PreCompute (transformnat-impl.h:708-763), one host thread per tower group
     auto build = [&](u32 t) {
         const u64 qt = q[t], ps = psi[t], psinv = invmod(ps, qt);
@@ -208,6 +208,12 @@ int ofhe_hip_plan_create(ofhe_ctx_t ctx, uint32_t log_n, uint32_t towers, const 
                         const size_t i = idx - N / 2;
                         itw3[e] = itwn[(size_t)t * N + 2 * i];
                         itw3[e + 1] = itwn[(size_t)t * N + 2 * i + 1];
+                        // same twiddle times R = 2^64 mod q for the fused Montgomery Hadamard
+                        const u64 R = (u64)(((u128)1 << 64) % qt);
+                        const u64 wr = mulmod(itw3[e], R, qt);
+                        const size_t er = (size_t)t * N + 2 * ((size_t)j * U3 + u);
+                        itw3r[er] = wr;
+                        itw3r[er + 1] = shoup_pre(wr, qt);
                     } else {
                         itw3[e] = TI[idx];
                         itw3[e + 1] = p->itab_pre[(size_t)t * N + idx];
@@ -224,6 +230,11 @@ int ofhe_hip_plan_create(ofhe_ctx_t ctx, uint32_t log_n, uint32_t towers, const 
         c.spq_sh = (mb >= 33 && (qt >> 32) == ((1ull << (mb - 32)) - 1)) ? mb - 32 : 0;
         c.nq = 0 - qt;
         c.nq4 = 0 - 4 * qt;
+        u64 inv = qt;  // q^-1 mod 2^64 by Newton iteration (q odd)
+        for (int it = 0; it < 6; it++) inv *= 2 - qt * inv;
+        c.qinv_neg = 0 - inv;
+        c.ninv_r = mulmod(ni, (u64)(((u128)1 << 64) % qt), qt);
+        c.ninv_r_pre = shoup_pre(c.ninv_r, qt);
         tc[t] = c;
     };
     {
@@ -253,6 +264,9 @@ int ofhe_hip_plan_create(ofhe_ctx_t ctx, uint32_t log_n, uint32_t towers, const 
         e = hipMemcpy(p->d_tw3, tw3.data(), sizeof(u64) * tw3.size(), hipMemcpyHostToDevice);
     if (e == hipSuccess && itw3.size())
         e = hipMemcpy(p->d_itw3, itw3.data(), sizeof(u64) * itw3.size(), hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMalloc(&p->d_itw3r, sizeof(u64) * (itw3r.size() ? itw3r.size() : 2));
+    if (e == hipSuccess && itw3r.size())
+        e = hipMemcpy(p->d_itw3r, itw3r.data(), sizeof(u64) * itw3r.size(), hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMalloc(&p->d_scal, sizeof(u64) * 2 * towers);
     if (e == hipSuccess) e = hipMemcpy(p->d_tc, tc.data(), sizeof(TowerConst) * towers, hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMemcpy(p->d_tw, tw.data(), sizeof(u64) * 2 * TN, hipMemcpyHostToDevice);
@@ -297,6 +311,7 @@ int ofhe_hip_plan_destroy(ofhe_plan_t p) {
     (void)hipFree(p->d_itwn);
     (void)hipFree(p->d_tw3);
     (void)hipFree(p->d_itw3);
+    (void)hipFree(p->d_itw3r);
     (void)hipFree(p->d_scal);
     delete p;
     return OFHE_OK;
@@ -329,6 +344,7 @@ static PlanArgs args_of(ofhe_plan_t p, u32 t0 = 0, u32 count = 0) {
     a.itwn = p->d_itwn + N * t0;
     a.tw3 = p->d_tw3 + (N >= 4096 ? (N / 16) * 30 * t0 : 0);
     a.itw3 = p->d_itw3 + (N >= 4096 ? (N / 16) * 30 * t0 : 0);
+    a.itw3r = p->d_itw3r + (N >= 4096 ? N * t0 : 0);
     a.sstride = a.dstride = a.bstride = N * count;
     a.scal = nullptr;
     a.log_n = p->log_n;
