@@ -120,7 +120,10 @@ __global__ __launch_bounds__(256) void k_bconv(BconvArgs A, const u64* __restric
 // ---------------------------------------------------------------------------
 constexpr u32 LIMB = 30;
 constexpr u64 LIMB_MASK = (1ull << LIMB) - 1;
-constexpr u32 BCONV_PT = 8;      // output towers per tile
+#ifndef OFHE_BCONV_PT
+#define OFHE_BCONV_PT 8
+#endif
+constexpr u32 BCONV_PT = OFHE_BCONV_PT;  // output towers per tile
 constexpr u32 BCONV_LIMB_QMAX = 16;
 
 __device__ __forceinline__ void limbs_to_u128(u64 a0, u64 a1, u64 a2, u64 a3, u64& lo, u64& hi) {
