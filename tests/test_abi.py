@@ -50,3 +50,35 @@ def test_kernels_built_for_gfx950():
 
     blob = open(ofhe_hip.LIB_PATH, "rb").read()
     assert b"gfx950" in blob
+
+
+def test_argument_errors_without_device():
+    """Entry points reject NULL / destroyed handles with a status code and a
+    thread-local message before touching the device (the OPENFHE_THROW analogue)."""
+    import ofhe_hip as H
+
+    L = H.lib()
+    vp = ctypes.c_void_p
+    null = vp()
+    q = (ctypes.c_uint64 * 2)(97, 193)
+    cases = [
+        L.ofhe_hip_init(0, None),
+        L.ofhe_hip_plan_create(null, 4, 1, q, q, ctypes.byref(vp())),
+        L.ofhe_hip_ks_create(null, 4, 1, q, q, 1, q, q, 1, ctypes.byref(vp())),
+        L.ofhe_hip_ntt_fwd(null, null, 1, null),
+        L.ofhe_hip_ntt_fwd_range(null, 0, 1, null, null, 16, 16, 1, null),
+        L.ofhe_hip_approx_mod_up(null, null, null, 1, null, null, 1, null),
+        L.ofhe_hip_approx_mod_down(null, null, null, q, 0, null, null, 1, null),
+        L.ofhe_hip_ks_core(null, 1, null, null, null, null, null, 0, 1, null),
+        L.ofhe_hip_ks_digits(null, 1, None, None),
+        L.ofhe_hip_automorphism(null, 3, 1, null, null, 1, null),
+        L.ofhe_hip_switch_modulus(null, null, null, 4, 97, 193, null),
+        L.ofhe_hip_alloc_async(null, 8, ctypes.byref(vp()), null),
+        L.ofhe_hip_bconv_create(null, 4, 1, 1, q, q, q, q, ctypes.byref(vp())),
+        L.ofhe_hip_plan_destroy(null),
+        L.ofhe_hip_ks_destroy(null),
+    ]
+    assert all(rc != 0 for rc in cases), cases
+    assert L.ofhe_hip_last_error()  # a message is set
+    with pytest.raises(H.MathError):
+        H._check(L.ofhe_hip_ntt_inv(null, null, 1, null))

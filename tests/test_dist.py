@@ -95,3 +95,59 @@ def test_two_rank_shard_and_broadcast():
     assert sorted(r[0] for r in res) == [0, 1]
     assert all(r[1] and r[2] for r in res), res
     assert all(r[3] == 2.0 for r in res)
+
+
+def _ks_worker(rank, world, port, q):
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        try:
+            import keyswitch as K
+            import oracle as O
+
+            # configs[4] in miniature: ciphertext batch sharded, the evaluation
+            # key generated on rank 0 and broadcast (bench.py --workload keyswitch)
+            log_n, sq, sp, dnum, GB = 5, 4, 2, 2, 4
+            n = 1 << log_n
+            m, r = O.moduli_chain(log_n, sq + sp)
+            kp = K.KeySwitchParams(n, m[:sq], r[:sq], m[sq:], r[sq:], dnum)
+            rng = np.random.default_rng(3)
+            c = np.stack([np.stack([rng.integers(0, x, size=n, dtype=np.uint64) for x in m[:sq]])
+                          for _ in range(GB)])
+            kb = torch.zeros((dnum, sq + sp, n), dtype=torch.int64)
+            ka = torch.zeros_like(kb)
+            if rank == 0:
+                krng = np.random.default_rng(11)
+                for t, x in enumerate(m):
+                    kb[:, t] = torch.from_numpy(krng.integers(0, x, size=(dnum, n), dtype=np.uint64).view(np.int64))
+                    ka[:, t] = torch.from_numpy(krng.integers(0, x, size=(dnum, n), dtype=np.uint64).view(np.int64))
+            shard.broadcast_evalkey(kb, src=0)
+            shard.broadcast_evalkey(ka, src=0)
+            kbn, kan = kb.numpy().view(np.uint64), ka.numpy().view(np.uint64)
+            start, count = shard.shard_batch(GB, rank, world)
+            o0, o1 = K.ks_core(kp, c[start:start + count], kbn, kan)
+            buf = [torch.zeros((2, count, sq, n), dtype=torch.int64) for _ in range(world)]
+            dist.all_gather(buf, torch.from_numpy(np.ascontiguousarray(np.stack([o0, o1])).view(np.int64)))
+            got = torch.cat(buf, dim=1).numpy().view(np.uint64)
+            r0, r1 = K.ks_core(kp, c, kbn, kan)
+            q.put((rank, bool(np.array_equal(got[0], r0) and np.array_equal(got[1], r1))))
+        finally:
+            dist.destroy_process_group()
+    except Exception as e:
+        q.put((rank, repr(e)))
+        raise
+
+
+def test_two_rank_sharded_keyswitch_with_broadcast_key():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_ks_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=180) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert sorted(r[0] for r in res) == [0, 1]
+    assert all(r[1] is True for r in res), res
