@@ -37,6 +37,31 @@ __device__ __forceinline__ u64 mad32(u32 a, u32 b, u64 c) { return (u64)a * (u64
 
 __device__ __forceinline__ u64 csub(u64 x, u64 m) { return x >= m ? x - m : x; }
 
+// csub for a wave-uniform m (held in SGPRs: the NTT kernels' per-tower
+// moduli).  The compiler emits v_cmp_u64 + 2 cndmask + sub/subb (5 VALU ops)
+// for csub; this selects on the borrow of the subtraction itself (sub_co,
+// subb_co, 2 cndmask on that vcc: 4 ops, no 64-bit compare, fewer VCC
+// hazard nops).  m MUST be uniform across the wave: an "s" operand of a
+// divergent value would be read from lane 0.
+#ifndef OFHE_CSUB_ASM
+#define OFHE_CSUB_ASM 1
+#endif
+__device__ __forceinline__ u64 csub_s(u64 x, u64 m) {
+#if OFHE_CSUB_ASM
+    u32 lo, hi;
+    asm("v_subrev_co_u32 %0, vcc, %4, %2\n\t"
+        "v_subbrev_co_u32 %1, vcc, %5, %3, vcc\n\t"
+        "v_cndmask_b32 %0, %0, %2, vcc\n\t"
+        "v_cndmask_b32 %1, %1, %3, vcc"
+        : "=&v"(lo), "=&v"(hi)
+        : "v"(lo32(x)), "v"(hi32(x)), "s"(lo32(m)), "v"(hi32(m))
+        : "vcc");
+    return pack(lo, hi);
+#else
+    return csub(x, m);
+#endif
+}
+
 // floor(a*b / 2^64) - e, e in {0, 1, 2}: drops a0*b0 and the carry of the
 // middle sum.
 #ifndef OFHE_QH_ADDC
@@ -133,20 +158,24 @@ __device__ __forceinline__ u64 barrett_ref(u64 a, u64 b, u64 q, u64 mu, u32 n_sh
     return r >= q ? r - q : r;
 }
 
-// Montgomery product a*b*2^-64 mod q in [0, 2q) for a*b < q*2^64 (here
-// a < 16q lazy, b < q canonical, q < 2^60): t = a*b, m = -t*q^-1 mod 2^64,
-// u = (t + m*q) / 2^64 exactly.  qinv_neg = -q^-1 mod 2^64.
-__device__ __forceinline__ u64 mont_mul(u64 a, u64 b, u64 q, u64 qinv_neg) {
-    u64 tl, th;
-    {
-        u64 p00 = mad32(lo32(a), lo32(b), 0);
-        u64 m1 = mad32(lo32(a), hi32(b), (u64)hi32(p00));
-        u64 m2 = mad32(hi32(a), lo32(b), (u64)lo32(m1));
-        th = mad32(hi32(a), hi32(b), (u64)hi32(m1)) + (u64)hi32(m2);
-        tl = ((u64)lo32(m2) << 32) | lo32(p00);
-    }
-    const u64 m = tl * qinv_neg;
-    return th + mulhi_exact(m, q) + (tl != 0);
+// Montgomery product a*b*2^-64 mod q in (0, 2q) for a < 12q (the lazy
+// forward output after a CS stage), b < q canonical, q < 2^60.
+//   t = a*b: with a < 1.5*2^63 and b1 = hi32(b) < 2^28 the two middle
+//     products and the carry word sum to < 2^64, so they chain through one
+//     64-bit accumulator (no zero-extended halves, no carry word);
+//   m = lo64(t) * q^-1 mod 2^64, so lo64(m*q) = lo64(t) and
+//   (t - m*q) / 2^64 = hi64(t) - hi64(m*q) exactly, in (-q, q): adding q
+//   gives (0, 2q) with no carry/borrow test on the low word.
+// qinv = q^-1 mod 2^64.
+__device__ __forceinline__ u64 mont_mul(u64 a, u64 b, u64 q, u64 qinv) {
+    const u64 x = mad32(lo32(a), lo32(b), 0);
+    const u64 y = mad32(hi32(a), lo32(b), x >> 32);  // < 1.5*2^63 + 2^32
+    const u64 z = mad32(lo32(a), hi32(b), y);        // + < 2^60: no wrap
+    const u64 th = mad32(hi32(a), hi32(b), z >> 32);
+    const u32 t0 = lo32(x), t1 = lo32(z);
+    const u64 m0 = mad32(t0, lo32(qinv), 0);
+    const u64 m = pack(lo32(m0), hi32(m0) + t0 * hi32(qinv) + t1 * lo32(qinv));
+    return th + q - mulhi_exact(m, q);
 }
 
 // Exact 64x64 -> 128 product (for base conversion accumulation).

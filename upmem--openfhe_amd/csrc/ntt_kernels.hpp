@@ -38,7 +38,7 @@ struct TowerConst {
     u64 nq4;       // 2^64 - 4q   the lazy adds back into carry-chain subtractions)
     u32 nshift;    // msb(q) - 2
     u32 spq_sh;    // msb(q) - 32 when q = 2^msb - d with d < 2^32, else 0
-    u64 qinv_neg;  // -q^-1 mod 2^64 (Montgomery Hadamard)
+    u64 qinv;      // q^-1 mod 2^64 (Montgomery Hadamard)
     u64 ninv_r;    // N^-1 * 2^64 mod q, and its Shoup precon: the fused
     u64 ninv_r_pre;//   pipeline's first inverse stage undoes the 2^-64
 };
@@ -149,9 +149,9 @@ __device__ __forceinline__ void ct_bfly_cs(u64& x, u64& y, Tw w, const Mod<SPQ>&
     const u64 t = shoup_lazy(y, w.w, w.wp, M);  // [0, 4q)
     u64 a;
     if (OFHE_LAZY_FWD)
-        a = cs ? ((SPQ && OFHE_THR) ? csub_thr8(x, M) : csub(x, M.q8)) : x;
+        a = cs ? ((SPQ && OFHE_THR) ? csub_thr8(x, M) : csub_s(x, M.q8)) : x;
     else
-        a = csub(x, M.q4);
+        a = csub_s(x, M.q4);
     x = a + t;
     y = a + M.q4 - t;
 }
@@ -165,7 +165,7 @@ template <class M_>
 __device__ __forceinline__ void gs_bfly(u64& x, u64& y, Tw w, const M_& M) {
     const u64 s = x + y;          // [0, 8q)
     const u64 d = x + M.q4 - y;   // (0, 8q)
-    x = csub(s, M.q4);
+    x = csub_s(s, M.q4);
     y = shoup_lazy(d, w.w, w.wp, M);  // [0, 4q)
 }
 
@@ -179,20 +179,20 @@ __device__ __forceinline__ void gs_bfly_ninv(u64& x, u64& y, Tw wn, u64 ninv, u6
 }
 
 __device__ __forceinline__ u64 canon8(u64 x, u64 q) {  // [0, 8q) -> [0, q)
-    x = csub(x, 4 * q);
-    x = csub(x, 2 * q);
-    return csub(x, q);
+    x = csub_s(x, 4 * q);
+    x = csub_s(x, 2 * q);
+    return csub_s(x, q);
 }
 // forward-transform output (any stage pattern) -> [0, q)
 template <bool SPQ>
 __device__ __forceinline__ u64 canon_fwd(u64 x, u64 q) {
-    if (SPQ && OFHE_THR) x = csub(x, 8 * q);  // [0, 2^(L+3) + 8q) -> [0, 8q + 8d)
-    if (OFHE_LAZY_FWD) x = csub(x, 8 * q);    // [0, 16q) -> [0, 8q)
+    if (SPQ && OFHE_THR) x = csub_s(x, 8 * q);  // [0, 2^(L+3) + 8q) -> [0, 8q + 8d)
+    if (OFHE_LAZY_FWD) x = csub_s(x, 8 * q);    // [0, 16q) -> [0, 8q)
     return canon8(x, q);
 }
 __device__ __forceinline__ u64 canon4(u64 x, u64 q) {  // [0, 4q) -> [0, q)
-    x = csub(x, 2 * q);
-    return csub(x, q);
+    x = csub_s(x, 2 * q);
+    return csub_s(x, q);
 }
 
 // ---------------------------------------------------------------------------
@@ -284,6 +284,8 @@ __device__ __forceinline__ void inv_round16(u64 (&v)[16], const u64* itw, u32 M0
 #define OFHE_COAL_B 1
 #endif
 constexpr bool kMontFused = OFHE_MONT && OFHE_TW3 && OFHE_COAL_B;
+// mont_mul takes a < 12q: the forward output after a CS stage (OFHE_THR widens it)
+static_assert(!(kMontFused && OFHE_THR), "Montgomery Hadamard needs the forward output < 12q");
 template <int S, class M_>
 __device__ __forceinline__ void fwd_stage16_t3(u64 (&v)[16], const u64* tw3, u32 U, u32 u, const M_& M) {
     constexpr int half = 8 >> S;
@@ -462,7 +464,7 @@ __global__ __launch_bounds__(256, OFHE_KB_WAVES) void k_block(PlanArgs P, const 
             wave_stage_in(bdat + boff + (tid >> 6) * 1024, lds, tid, bb);
             if (kMontFused) {
 #pragma unroll
-                for (int k = 0; k < 16; k++) v[k] = mont_mul(v[k], bb[k], q, tc.qinv_neg);  // [0, 2q)
+                for (int k = 0; k < 16; k++) v[k] = mont_mul(v[k], bb[k], q, tc.qinv);  // (0, 2q)
             } else {
 #pragma unroll
                 for (int k = 0; k < 16; k++) v[k] = barrett_ref(v[k], bb[k], q, tc.mu, tc.nshift);

@@ -232,7 +232,7 @@ int ofhe_hip_plan_create(ofhe_ctx_t ctx, uint32_t log_n, uint32_t towers, const 
         c.nq4 = 0 - 4 * qt;
         u64 inv = qt;  // q^-1 mod 2^64 by Newton iteration (q odd)
         for (int it = 0; it < 6; it++) inv *= 2 - qt * inv;
-        c.qinv_neg = 0 - inv;
+        c.qinv = inv;
         c.ninv_r = mulmod(ni, (u64)(((u128)1 << 64) % qt), qt);
         c.ninv_r_pre = shoup_pre(c.ninv_r, qt);
         tc[t] = c;
