@@ -328,6 +328,33 @@ def test_special_prime_switch_identical(hip, O, monkeypatch):
     assert np.array_equal(outs[0], O.ntt_mul_intt(a, b, O.Tables(n, qs, rs)))
 
 
+def test_split4_identical(hip, O, monkeypatch):
+    """N = 2^16 under OFHE_SPLIT4 (4 column stages + a 12-stage block pass, so
+    the inverse block twist covers groups of 4096 instead of 256) gives the
+    same canonical results as the default 8 | 8 split."""
+    import torch
+
+    H, ctx = hip
+    log_n, T, B = 16, 3, 2
+    n = 1 << log_n
+    qs, rs = O.moduli_chain(log_n, T)
+    tb = O.Tables(n, qs, rs)
+    a = O.uniform_dcrt(B, T, n, qs, 7)
+    b = O.uniform_dcrt(B, T, n, qs, 8)
+    want_pipe, want_inv = O.ntt_mul_intt(a, b, tb), O.ntt_inv(a, tb)
+    for env in (None, "1"):
+        if env:
+            monkeypatch.setenv("OFHE_SPLIT4", env)
+        plan = H.NTTPlan(ctx, log_n, qs, rs)
+        xa, xb = dev(a), dev(b)
+        xc = torch.empty_like(xa)
+        plan.ntt_mul_intt(xa.data_ptr(), xb.data_ptr(), xc.data_ptr(), B, stream())
+        xi = dev(a)
+        plan.inverse(xi.data_ptr(), B, stream())
+        assert np.array_equal(host(xc), want_pipe), env
+        assert np.array_equal(host(xi), want_inv), env
+
+
 def test_stream_ordered_alloc_and_zero(hip):
     """ofhe_hip_alloc_async / free_async / zero on a caller stream."""
     import torch

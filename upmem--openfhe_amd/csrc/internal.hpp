@@ -88,10 +88,10 @@ struct ofhe_plan_s {
     ofhe::TowerConst* d_tc = nullptr;
     ofhe::u64* d_tw = nullptr;
     ofhe::u64* d_itw = nullptr;
-    ofhe::u64* d_itwn = nullptr;
     ofhe::u64* d_tw3 = nullptr;   // round-3 transposed twiddles (log_n >= 12)
-    ofhe::u64* d_itw3 = nullptr;
-    ofhe::u64* d_itw3r = nullptr;  // t = 1 section of d_itw3 times 2^64 mod q (fused Montgomery Hadamard)
+    ofhe::u64* d_dtw = nullptr;     // DIT inverse twiddles of the block pass
+    ofhe::u64* d_twist = nullptr;   // block-pass inverse twist N^-1 psi^-((2 rev(b) + 1) j0)
+    ofhe::u64* d_twist_r = nullptr; // the same times 2^64 mod q (fused pipeline, Montgomery Hadamard)
     // host copies (for ofhe_hip_plan_tables and scalar prep)
     std::vector<ofhe::u64> q, psi, tab, tab_pre, itab, itab_pre, ninv;
     ofhe::u64* d_scal = nullptr;  // scratch for per-tower scalars (modmul_scalar)

@@ -39,8 +39,6 @@ struct TowerConst {
     u32 nshift;    // msb(q) - 2
     u32 spq_sh;    // msb(q) - 32 when q = 2^msb - d with d < 2^32, else 0
     u64 qinv;      // q^-1 mod 2^64 (Montgomery Hadamard)
-    u64 ninv_r;    // N^-1 * 2^64 mod q, and its Shoup precon: the fused
-    u64 ninv_r_pre;//   pipeline's first inverse stage undoes the 2^-64
 };
 template <bool SPQ>
 __device__ __forceinline__ Mod<SPQ> load_mod(const TowerConst& tc) {
@@ -52,15 +50,14 @@ __device__ __forceinline__ Mod<SPQ> load_mod(const TowerConst& tc) {
 struct PlanArgs {
     const TowerConst* tc;  // [T]
     const u64* tw;         // [T][N][2]   forward Table (bit-reversed powers of psi)
-    const u64* itw;        // [T][N][2]   inverse TableI
-    const u64* itwn;       // [T][N/2][2] TableI[N/2 + i] * N^-1 (first inverse stage)
+    const u64* itw;        // [T][N][2]   inverse TableI (GS column passes)
     const u64* tw3;        // [T][15N/16][2] round-3 forward twiddles, lane-contiguous (log_n >= 12)
-    const u64* itw3;       // [T][15N/16][2] round-3 inverse twiddles (stage t = 1 with N^-1)
-    const u64* itw3r;      // [T][N/2][2] the t = 1 section of itw3 times 2^64 mod q (fused, OFHE_MONT)
     u64 sstride;           // words between batch entries of src (towers * N when dense)
     u64 dstride;           // words between batch entries of dst (and of the Hadamard operand)
     u64 bstride;           // words between batch entries of the second operand (bdat)
     const u64* scal;       // MODE_FWD_SUB: [towers][3] = (q, s, s') per tower of the range
+    const u64* dtw;        // [T][N][2]   DIT inverse twiddles: dtw[t + k] = psi^(-k N / t), k < t
+    const u64* twist;      // [T][N][2]   output twist N^-1 psi^-j (times 2^64 mod q for the fused pipeline)
     u32 log_n;
     u32 towers;            // towers in this launch (a plan range starts at tc[0])
 };
@@ -169,15 +166,6 @@ __device__ __forceinline__ void gs_bfly(u64& x, u64& y, Tw w, const M_& M) {
     y = shoup_lazy(d, w.w, w.wp, M);  // [0, 4q)
 }
 
-// First inverse stage (t = 1) with N^-1 folded in: both outputs scaled.
-template <class M_>
-__device__ __forceinline__ void gs_bfly_ninv(u64& x, u64& y, Tw wn, u64 ninv, u64 ninv_pre, const M_& M) {
-    const u64 s = x + y;
-    const u64 d = x + M.q4 - y;
-    x = shoup_lazy(s, ninv, ninv_pre, M);
-    y = shoup_lazy(d, wn.w, wn.wp, M);
-}
-
 __device__ __forceinline__ u64 canon8(u64 x, u64 q) {  // [0, 8q) -> [0, q)
     x = csub_s(x, 4 * q);
     x = csub_s(x, 2 * q);
@@ -193,6 +181,100 @@ __device__ __forceinline__ u64 canon_fwd(u64 x, u64 q) {
 __device__ __forceinline__ u64 canon4(u64 x, u64 q) {  // [0, 4q) -> [0, q)
     x = csub_s(x, 2 * q);
     return csub_s(x, q);
+}
+
+// ---------------------------------------------------------------------------
+// Inverse transform as a cyclic decimation-in-time NTT plus an output twist
+// The reference's inverse (GS, transformnat-impl.h:492-552) is
+//   a_j = N^-1 psi^-j sum_k Y[k] omega^-kj,   omega = psi^2, Y[k] = y[rev(k)],
+// and the sum over the bit-reversed input y is the textbook iterative
+// Cooley-Tukey DIT: stages t = 1, 2, ..., N/2 pair (e, e + t) as
+// (x + w y, x - w y) with w = psi^(-(e mod t) N / t) = dtw[t + e mod t].
+// Compared with the merged-twist GS form this
+//   * uses the cheaper CT butterfly (lazy, alternating reduction as forward);
+//   * has trivial twiddles (w = 1) at e mod t = 0: every butterfly of stage
+//     t = 1, half of t = 2, ... -- and in the block pass's last round (t <= 8)
+//     they sit at fixed register positions, so they cost two adds;
+//   * gives that round wave-uniform twiddles (11 scalars per tower);
+// The block pass runs the DIT stages inside its groups of G = 2^lb elements
+// (lb = 8 under split8, else min(12, logN)); the GS column pass (unchanged)
+// runs the rest.  They meet because the GS intermediate after its first lb
+// stages is, for group b and position j0 (checked numerically),
+//   W_b[j0] = psi^-((2 rev(b) + 1) j0) * Z_b[j0],
+// Z_b = the group's cyclic DIT output, rev over logN - lb bits; so the block
+// pass ends with the per-element twist N^-1 psi^-((2 rev(b) + 1) j0) (N^-1
+// moves here from GS's first stage; for G = N it is N^-1 psi^-j).  Same
+// canonical outputs, bit for bit.
+// ---------------------------------------------------------------------------
+static_assert(OFHE_LAZY_FWD, "the DIT inverse uses the alternating lazy CT butterflies");
+
+// x + y and x + B q - y for y < B q (B q passed as bq): the w = 1 butterfly
+__device__ __forceinline__ void triv_bfly(u64& x, u64& y, u64 bq) {
+    const u64 s = x + y;
+    y = x + bq - y;
+    x = s;
+}
+
+// DIT stage of a radix-16 register round with element stride st: the thread
+// holds v[k] = x[p0 + k st], r = p0 mod st; half = 2^H pairs (k, k + half),
+// twiddle index st half + r + st (k mod half) -- base points at entry
+// st half + r.  CS: conditional-subtract stage (inputs < 16q, else < 12q).
+template <int H, int CS, class M_>
+__device__ __forceinline__ void dit_stage16(u64 (&v)[16], const u64* base, u32 st, const M_& M) {
+    constexpr int half = 1 << H;
+#pragma unroll
+    for (int j = 0; j < half; j++) {
+        const Tw w = ldtw(base, st * j);
+#pragma unroll
+        for (int g = 0; g < 16; g += 2 * half) ct_bfly<CS>(v[g + j], v[g + j + half], w, M);
+    }
+}
+template <class M_>
+__device__ __forceinline__ void dit_round16(u64 (&v)[16], const u64* dtw, u32 st, u32 r, const M_& M) {
+    dit_stage16<0, 1>(v, dtw + 2 * ((u64)st + r), st, M);
+    dit_stage16<1, 0>(v, dtw + 2 * ((u64)2 * st + r), st, M);
+    dit_stage16<2, 1>(v, dtw + 2 * ((u64)4 * st + r), st, M);
+    dit_stage16<3, 0>(v, dtw + 2 * ((u64)8 * st + r), st, M);
+}
+
+// The first four DIT stages (t = 1, 2, 4, 8) on 16 consecutive elements, inputs
+// < 2q (the Montgomery Hadamard's (0, 2q) or canonical data): twiddles
+// dtw[t + j] are the same for every thread, j = 0 is w = 1.
+//   t = 1: all trivial, -> < 4q;  t = 2: -> < 8q;  t = 4: -> < 16q (trivial)
+//   / < 12q;  t = 8: conditional subtract first, -> < 16q.
+template <bool SPQ>
+__device__ __forceinline__ void dit_round3(u64 (&v)[16], const u64* dtw, const Mod<SPQ>& M) {
+#pragma unroll
+    for (int g = 0; g < 16; g += 2) triv_bfly(v[g], v[g + 1], 2 * M.q);
+#pragma unroll
+    for (int g = 0; g < 16; g += 4) triv_bfly(v[g], v[g + 2], M.q4);
+    {
+        const Tw w = ldtw(dtw, 3);
+#pragma unroll
+        for (int g = 0; g < 16; g += 4) ct_bfly<0>(v[g + 1], v[g + 3], w, M);
+    }
+#pragma unroll
+    for (int g = 0; g < 16; g += 8) triv_bfly(v[g], v[g + 4], M.q8);
+#pragma unroll
+    for (int j = 1; j < 4; j++) {
+        const Tw w = ldtw(dtw, 4 + j);
+#pragma unroll
+        for (int g = 0; g < 16; g += 8) ct_bfly<0>(v[g + j], v[g + j + 4], w, M);
+    }
+    {
+        const u64 a = csub_s(v[0], M.q8), b = csub_s(v[8], M.q8);
+        v[0] = a;
+        v[8] = b;
+        triv_bfly(v[0], v[8], M.q8);
+    }
+#pragma unroll
+    for (int j = 1; j < 8; j++) ct_bfly<1>(v[j], v[j + 8], ldtw(dtw, 8 + j), M);
+}
+
+// last step of every inverse: x * N^-1 psi^-j (the twist entry f) -> [0, q)
+template <bool SPQ>
+__device__ __forceinline__ u64 twist_out(u64 x, Tw f, const Mod<SPQ>& M) {
+    return canon4(shoup_lazy(x, f.w, f.wp, M), M.q);
 }
 
 // ---------------------------------------------------------------------------
@@ -225,19 +307,6 @@ __device__ __forceinline__ void inv_stage16(u64 (&v)[16], const u64* itw, u32 M0
     }
 }
 
-// last inverse round stage s = 3 at global t = 1: uses the N^-1-folded table.
-// itwn is indexed by i = (M0 << 3) + j - N/2.
-template <class M_>
-__device__ __forceinline__ void inv_stage16_first(u64 (&v)[16], const u64* itwn, u32 i0, const TowerConst& tc,
-                                                  const M_& M) {
-    const u64* base = itwn + 2 * (u64)i0;
-#pragma unroll
-    for (int j = 0; j < 8; j++) {
-        Tw w = ldtw(base, j);
-        gs_bfly_ninv(v[2 * j], v[2 * j + 1], w, tc.ninv, tc.ninv_pre, M);
-    }
-}
-
 template <class M_>
 __device__ __forceinline__ void fwd_round16(u64 (&v)[16], const u64* tw, u32 M0, const M_& M) {
     fwd_stage16<0>(v, tw, M0, M);
@@ -265,10 +334,10 @@ __device__ __forceinline__ void inv_round16(u64 (&v)[16], const u64* itw, u32 M0
 #ifndef OFHE_TW3
 #define OFHE_TW3 1
 #endif
-// OFHE_MONT (needs OFHE_TW3): the fused pipeline's Hadamard is a Montgomery
-// product on the lazy forward output (no canonicalisation, no Barrett), and
-// the 2^-64 it introduces is cancelled by 2^64 folded into the first inverse
-// stage's N^-1 twiddles.  Intermediate values differ in representation only;
+// OFHE_MONT: the fused pipeline's Hadamard is a Montgomery product on the lazy
+// forward output (no canonicalisation, no Barrett), and the 2^-64 it
+// introduces is cancelled by 2^64 folded into the inverse's N^-1 twist
+// (PlanArgs::twist = the plan's twist_r table).  Intermediate values differ in representation only;
 // the canonical output is the same integer.
 #ifndef OFHE_MONT
 #define OFHE_MONT 1
@@ -283,7 +352,7 @@ __device__ __forceinline__ void inv_round16(u64 (&v)[16], const u64* itw, u32 M0
 #ifndef OFHE_COAL_B
 #define OFHE_COAL_B 1
 #endif
-constexpr bool kMontFused = OFHE_MONT && OFHE_TW3 && OFHE_COAL_B;
+constexpr bool kMontFused = OFHE_MONT && OFHE_COAL_B;
 // mont_mul takes a < 12q: the forward output after a CS stage (OFHE_THR widens it)
 static_assert(!(kMontFused && OFHE_THR), "Montgomery Hadamard needs the forward output < 12q");
 template <int S, class M_>
@@ -297,24 +366,6 @@ __device__ __forceinline__ void fwd_stage16_t3(u64 (&v)[16], const u64* tw3, u32
         for (int k = j * 2 * half; k < j * 2 * half + half; k++) ct_bfly<S & 1>(v[k], v[k + half], w, M);
     }
 }
-// base = this stage's section (itw3 + 2 (2^S - 1) U, or itw3r for S = 3)
-template <int S, class M_>
-__device__ __forceinline__ void inv_stage16_t3(u64 (&v)[16], const u64* base, u32 U, u32 u, u64 ninv, u64 ninv_pre,
-                                               const M_& M) {
-    constexpr int half = 8 >> S;
-#pragma unroll
-    for (int j = 0; j < (1 << S); j++) {
-        Tw w = ldtw(base + 2 * (u64)j * U, u);
-#pragma unroll
-        for (int k = j * 2 * half; k < j * 2 * half + half; k++) {
-            if (S == 3)
-                gs_bfly_ninv(v[k], v[k + half], w, ninv, ninv_pre, M);
-            else
-                gs_bfly(v[k], v[k + half], w, M);
-        }
-    }
-}
-
 // LDS placement of block element p: one u64 of padding per 16 elements.  It is
 // additive, so every round addresses its 16 values as one base register plus
 // immediate offsets, and it is bank-conflict free for the round-2/3 patterns
@@ -390,8 +441,6 @@ __global__ __launch_bounds__(256, OFHE_KB_WAVES) void k_block(PlanArgs P, const 
     const u64 q = tc.q;
     const Mod<SPQ> M = load_mod<SPQ>(tc);
     const u64* tw = P.tw + (u64)t * N * 2;
-    const u64* itw = P.itw + (u64)t * N * 2;
-    const u64* itwn = P.itwn + (u64)t * N;  // N/2 pairs
     const u32 h = tid >> 4, r = tid & 15;
     // padded LDS bases (lds_pad(p) = p + p/16) of the three round layouts
     const u32 L1 = tid + h;      // lds_pad(tid + 256 k)      = L1 + 272 k
@@ -496,33 +545,28 @@ __global__ __launch_bounds__(256, OFHE_KB_WAVES) void k_block(PlanArgs P, const 
             }
         }
     }
-    // inverse round 3': st = 1, GS stages t = 1, 2, 4, 8 (s = 3, 2, 1, 0)
-    if (OFHE_TW3) {
-        const u64* itw3 = P.itw3 + (u64)t * (N / 16) * 30;
-        const u32 U = N >> 4, u = g * 256 + tid;
-        if (MODE == MODE_FUSED && kMontFused)  // undo the Montgomery 2^-64 with the N^-1 fold
-            inv_stage16_t3<3>(v, P.itw3r + (u64)t * N, U, u, tc.ninv_r, tc.ninv_r_pre, M);
-        else
-            inv_stage16_t3<3>(v, itw3 + 2 * (u64)7 * U, U, u, tc.ninv, tc.ninv_pre, M);
-        inv_stage16_t3<2>(v, itw3 + 2 * (u64)3 * U, U, u, 0, 0, M);
-        inv_stage16_t3<1>(v, itw3 + 2 * (u64)1 * U, U, u, 0, 0, M);
-        inv_stage16_t3<0>(v, itw3, U, u, 0, 0, M);
-    } else {
-        const u32 M0 = (N >> 4) + g * 256 + tid;
-        inv_stage16_first(v, itwn, (M0 << 3) - (N >> 1), tc, M);
-        inv_stage16<2>(v, itw, M0, M);
-        inv_stage16<1>(v, itw, M0, M);
-        inv_stage16<0>(v, itw, M0, M);
-    }
+    // inverse as DIT inside the block's groups: round 3' (t = 1..8, uniform
+    // twiddles), round 2' (t = 16..128, st = 16, r = tid & 15), round 1'
+    // (NR = 3: t = 256..2048, st = 256, r = tid), then the twist (group b =
+    // position / G): canonical when the block ran every stage (N = 2^12),
+    // else lazy [0, 4q) for the GS column pass
+    const u64* dtw = P.dtw + (u64)t * N * 2;
+    dit_round3(v, dtw, M);
 #pragma unroll
     for (int k = 0; k < 16; k++) lds[L3 + k] = v[k];
     __syncthreads();
 #pragma unroll
     for (int k = 0; k < 16; k++) v[k] = lds[L2 + 17 * k];
-    inv_round16(v, itw, (N >> 8) + g * 16 + h, M);
+    dit_round16(v, dtw, 16, r, M);
+    const u64* tw_ = P.twist + (u64)t * N * 2 + 2 * ((u64)g << 12);
     if (NR == 2) {
+        // twist into the GS column pass's input, lazy [0, 4q)
 #pragma unroll
-        for (int k = 0; k < 16; k++) st_s(oblk + h * 256 + r + 16 * k, v[k]);
+        for (int k = 0; k < 16; k++) {
+            const u32 p = h * 256 + r + 16 * k;
+            const Tw f = ldtw(tw_, p);
+            st_s(oblk + p, shoup_lazy(v[k], f.w, f.wp, M));
+        }
         return;
     }
 #pragma unroll
@@ -530,10 +574,11 @@ __global__ __launch_bounds__(256, OFHE_KB_WAVES) void k_block(PlanArgs P, const 
     __syncthreads();
 #pragma unroll
     for (int k = 0; k < 16; k++) v[k] = lds[L1 + 272 * k];
-    inv_round16(v, itw, (N >> 12) + g, M);
-    if (logn == 12) {
+    dit_round16(v, dtw, 256, tid, M);
 #pragma unroll
-        for (int k = 0; k < 16; k++) v[k] = canon4(v[k], q);
+    for (int k = 0; k < 16; k++) {
+        const Tw f = ldtw(tw_, tid + 256 * k);
+        v[k] = logn == 12 ? twist_out(v[k], f, M) : shoup_lazy(v[k], f.w, f.wp, M);
     }
 #pragma unroll
     for (int k = 0; k < 16; k++) st_s(oblk + tid + 256 * k, v[k]);
@@ -702,8 +747,6 @@ __global__ __launch_bounds__(256) void k_small(PlanArgs P, const u64* src, u64* 
     const u64 q = tc.q;
     const Mod<SPQ> M = load_mod<SPQ>(tc);
     const u64* tw = P.tw + (u64)t * N * 2;
-    const u64* itw = P.itw + (u64)t * N * 2;
-    const u64* itwn = P.itwn + (u64)t * N;
     (void)batch;
     for (u32 i = threadIdx.x; i < N; i += blockDim.x) lds[i] = src[soff + i];
     __syncthreads();
@@ -730,21 +773,20 @@ __global__ __launch_bounds__(256) void k_small(PlanArgs P, const u64* src, u64* 
             return;
         }
     }
-    for (u32 m = half, lt = 0; m >= 1; m >>= 1, lt++) {
+    const u64* dtw = P.dtw + (u64)t * N * 2;
+    for (u32 lt = 0; lt < logn; lt++) {
         const u32 tt = 1u << lt;
         for (u32 k = threadIdx.x; k < half; k += blockDim.x) {
-            const u32 i = k >> lt, j = (i << (lt + 1)) + (k & (tt - 1));
+            const u32 i = k >> lt, e = k & (tt - 1), j = (i << (lt + 1)) + e;
             u64 x = lds[j], y = lds[j + tt];
-            if (m == half)
-                gs_bfly_ninv(x, y, ldtw(itwn, i), tc.ninv, tc.ninv_pre, M);
-            else
-                gs_bfly(x, y, ldtw(itw, m + i), M);
+            ct_bfly<1>(x, y, ldtw(dtw, tt + e), M);
             lds[j] = x;
             lds[j + tt] = y;
         }
         __syncthreads();
     }
-    for (u32 i = threadIdx.x; i < N; i += blockDim.x) dst[off + i] = canon4(lds[i], q);
+    const u64* tw_ = P.twist + (u64)t * N * 2;
+    for (u32 i = threadIdx.x; i < N; i += blockDim.x) dst[off + i] = twist_out(lds[i], ldtw(tw_, i), M);
 }
 
 }  // namespace ofhe

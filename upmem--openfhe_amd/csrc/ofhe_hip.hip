@@ -162,12 +162,16 @@ int ofhe_hip_plan_create(ofhe_ctx_t ctx, uint32_t log_n, uint32_t towers, const 
     p->itab_pre.resize(TN);
     p->ninv.resize(towers);
     std::vector<TowerConst> tc(towers);
-    std::vector<u64> tw(2 * TN), itw(2 * TN), itwn(TN);
+    std::vector<u64> tw(2 * TN), itw(2 * TN);
     // round-3 transposed tables (k_block, see ntt_kernels.hpp): per tower
     // 15 U pairs, U = N/16, entry (S, j, u) at (2^S - 1) U + j U + u
     const u32 U3 = N >= 4096 ? N / 16 : 0;
     const size_t W3 = (size_t)15 * U3 * 2;  // words per tower
-    std::vector<u64> tw3(W3 * towers), itw3(W3 * towers), itw3r((size_t)(U3 ? N : 0) * towers);
+    std::vector<u64> tw3(W3 * towers);
+    // DIT inverse (ntt_kernels.hpp): dtw[t + k] = psi^(-k N / t) for t = 1..N/2,
+    // k < t; the block pass's output twist, and twist_r = twist * 2^64 mod q
+    std::vector<u64> dtw(2 * TN), twist(2 * TN), twist_r(2 * TN);
+    const bool split8 = log_n == 16 && !getenv("OFHE_SPLIT4");
     // PreCompute (transformnat-impl.h:708-763), one host thread per tower group
     auto build = [&](u32 t) {
         const u64 qt = q[t], ps = psi[t], psinv = invmod(ps, qt);
@@ -192,11 +196,6 @@ int ofhe_hip_plan_create(ofhe_ctx_t ctx, uint32_t log_n, uint32_t towers, const 
             itw[2 * k] = TI[i];
             itw[2 * k + 1] = p->itab_pre[k];
         }
-        for (u32 i = 0; i < N / 2; i++) {
-            const u64 w = mulmod(TI[N / 2 + i], ni, qt);
-            itwn[(size_t)t * N + 2 * i] = w;
-            itwn[(size_t)t * N + 2 * i + 1] = shoup_pre(w, qt);
-        }
         for (u32 S = 0; S < 4 && U3; S++)
             for (u32 j = 0; j < (1u << S); j++)
                 for (u32 u = 0; u < U3; u++) {
@@ -204,21 +203,40 @@ int ofhe_hip_plan_create(ofhe_ctx_t ctx, uint32_t log_n, uint32_t towers, const 
                     const u32 idx = ((U3 + u) << S) + j;
                     tw3[e] = T[idx];
                     tw3[e + 1] = p->tab_pre[(size_t)t * N + idx];
-                    if (S == 3) {  // first inverse stage, N^-1 folded (itwn)
-                        const size_t i = idx - N / 2;
-                        itw3[e] = itwn[(size_t)t * N + 2 * i];
-                        itw3[e + 1] = itwn[(size_t)t * N + 2 * i + 1];
-                        // same twiddle times R = 2^64 mod q for the fused Montgomery Hadamard
-                        const u64 R = (u64)(((u128)1 << 64) % qt);
-                        const u64 wr = mulmod(itw3[e], R, qt);
-                        const size_t er = (size_t)t * N + 2 * ((size_t)j * U3 + u);
-                        itw3r[er] = wr;
-                        itw3r[er + 1] = shoup_pre(wr, qt);
-                    } else {
-                        itw3[e] = TI[idx];
-                        itw3[e + 1] = p->itab_pre[(size_t)t * N + idx];
-                    }
                 }
+        {
+            u64* D = &dtw[2 * (size_t)t * N];
+            u64* F = &twist[2 * (size_t)t * N];
+            u64* FR = &twist_r[2 * (size_t)t * N];
+            D[0] = 1;
+            D[1] = shoup_pre(1, qt);
+            for (u32 tt = 1; tt < N; tt <<= 1) {
+                const u64 base = powmod(psinv, N / tt, qt);
+                u64 w = 1;
+                for (u32 k = 0; k < tt; k++) {
+                    D[2 * (tt + k)] = w;
+                    D[2 * (tt + k) + 1] = shoup_pre(w, qt);
+                    w = mulmod(w, base, qt);
+                }
+            }
+            // block-pass twist: group b of G = 2^lb, position j0 ->
+            // N^-1 psi^-((2 rev(b) + 1) j0) (ntt_kernels.hpp)
+            const u32 lb = split8 ? 8 : (log_n < 12 ? log_n : 12), G = 1u << lb;
+            const u64 R = (u64)(((u128)1 << 64) % qt);
+            for (u32 b = 0; b < N / G; b++) {
+                const u64 step = powmod(psinv, 2 * (u64)bitrev(b, log_n - lb) + 1, qt);
+                u64 f = ni;
+                for (u32 j0 = 0; j0 < G; j0++) {
+                    const u32 j = b * G + j0;
+                    F[2 * j] = f;
+                    F[2 * j + 1] = shoup_pre(f, qt);
+                    const u64 fr = mulmod(f, R, qt);
+                    FR[2 * j] = fr;
+                    FR[2 * j + 1] = shoup_pre(fr, qt);
+                    f = mulmod(f, step, qt);
+                }
+            }
+        }
         TowerConst c{};
         c.q = qt;
         c.ninv = ni;
@@ -233,8 +251,6 @@ int ofhe_hip_plan_create(ofhe_ctx_t ctx, uint32_t log_n, uint32_t towers, const 
         u64 inv = qt;  // q^-1 mod 2^64 by Newton iteration (q odd)
         for (int it = 0; it < 6; it++) inv *= 2 - qt * inv;
         c.qinv = inv;
-        c.ninv_r = mulmod(ni, (u64)(((u128)1 << 64) % qt), qt);
-        c.ninv_r_pre = shoup_pre(c.ninv_r, qt);
         tc[t] = c;
     };
     {
@@ -252,26 +268,24 @@ int ofhe_hip_plan_create(ofhe_ctx_t ctx, uint32_t log_n, uint32_t towers, const 
     p->spq = true;
     for (u32 t = 0; t < towers; t++) p->spq = p->spq && tc[t].spq_sh != 0;
     if (getenv("OFHE_NO_SPQ")) p->spq = false;  // A/B switch for tests and timing
-    p->split8 = log_n == 16 && !getenv("OFHE_SPLIT4");
+    p->split8 = split8;
     hipError_t e = hipSetDevice(ctx->device);
     if (e == hipSuccess) e = hipMalloc(&p->d_tc, sizeof(TowerConst) * towers);
     if (e == hipSuccess) e = hipMalloc(&p->d_tw, sizeof(u64) * 2 * TN);
     if (e == hipSuccess) e = hipMalloc(&p->d_itw, sizeof(u64) * 2 * TN);
-    if (e == hipSuccess) e = hipMalloc(&p->d_itwn, sizeof(u64) * TN);
     if (e == hipSuccess) e = hipMalloc(&p->d_tw3, sizeof(u64) * (tw3.size() ? tw3.size() : 2));
-    if (e == hipSuccess) e = hipMalloc(&p->d_itw3, sizeof(u64) * (itw3.size() ? itw3.size() : 2));
     if (e == hipSuccess && tw3.size())
         e = hipMemcpy(p->d_tw3, tw3.data(), sizeof(u64) * tw3.size(), hipMemcpyHostToDevice);
-    if (e == hipSuccess && itw3.size())
-        e = hipMemcpy(p->d_itw3, itw3.data(), sizeof(u64) * itw3.size(), hipMemcpyHostToDevice);
-    if (e == hipSuccess) e = hipMalloc(&p->d_itw3r, sizeof(u64) * (itw3r.size() ? itw3r.size() : 2));
-    if (e == hipSuccess && itw3r.size())
-        e = hipMemcpy(p->d_itw3r, itw3r.data(), sizeof(u64) * itw3r.size(), hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMalloc(&p->d_dtw, sizeof(u64) * 2 * TN);
+    if (e == hipSuccess) e = hipMalloc(&p->d_twist, sizeof(u64) * 2 * TN);
+    if (e == hipSuccess) e = hipMalloc(&p->d_twist_r, sizeof(u64) * 2 * TN);
+    if (e == hipSuccess) e = hipMemcpy(p->d_dtw, dtw.data(), sizeof(u64) * 2 * TN, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(p->d_twist, twist.data(), sizeof(u64) * 2 * TN, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(p->d_twist_r, twist_r.data(), sizeof(u64) * 2 * TN, hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMalloc(&p->d_scal, sizeof(u64) * 2 * towers);
     if (e == hipSuccess) e = hipMemcpy(p->d_tc, tc.data(), sizeof(TowerConst) * towers, hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMemcpy(p->d_tw, tw.data(), sizeof(u64) * 2 * TN, hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMemcpy(p->d_itw, itw.data(), sizeof(u64) * 2 * TN, hipMemcpyHostToDevice);
-    if (e == hipSuccess) e = hipMemcpy(p->d_itwn, itwn.data(), sizeof(u64) * TN, hipMemcpyHostToDevice);
     if (e != hipSuccess) {
         ofhe_hip_plan_destroy(p);
         return fail(OFHE_ERR_HIP, std::string("plan upload: ") + hipGetErrorString(e));
@@ -308,10 +322,10 @@ int ofhe_hip_plan_destroy(ofhe_plan_t p) {
     (void)hipFree(p->d_tc);
     (void)hipFree(p->d_tw);
     (void)hipFree(p->d_itw);
-    (void)hipFree(p->d_itwn);
     (void)hipFree(p->d_tw3);
-    (void)hipFree(p->d_itw3);
-    (void)hipFree(p->d_itw3r);
+    (void)hipFree(p->d_dtw);
+    (void)hipFree(p->d_twist);
+    (void)hipFree(p->d_twist_r);
     (void)hipFree(p->d_scal);
     delete p;
     return OFHE_OK;
@@ -341,14 +355,21 @@ static PlanArgs args_of(ofhe_plan_t p, u32 t0 = 0, u32 count = 0) {
     a.tc = p->d_tc + t0;
     a.tw = p->d_tw + 2 * N * t0;
     a.itw = p->d_itw + 2 * N * t0;
-    a.itwn = p->d_itwn + N * t0;
     a.tw3 = p->d_tw3 + (N >= 4096 ? (N / 16) * 30 * t0 : 0);
-    a.itw3 = p->d_itw3 + (N >= 4096 ? (N / 16) * 30 * t0 : 0);
-    a.itw3r = p->d_itw3r + (N >= 4096 ? N * t0 : 0);
     a.sstride = a.dstride = a.bstride = N * count;
     a.scal = nullptr;
+    a.dtw = p->d_dtw + 2 * N * t0;
+    a.twist = p->d_twist + 2 * N * t0;
     a.log_n = p->log_n;
     a.towers = count;
+    return a;
+}
+
+// Fused pipeline: with the Montgomery Hadamard (kMontFused, log_n >= 12) the
+// inverse output twist also carries 2^64 to cancel its 2^-64.
+static PlanArgs fused_args(ofhe_plan_t p) {
+    PlanArgs a = args_of(p);
+    if (kMontFused && p->log_n >= 12) a.twist = p->d_twist_r;
     return a;
 }
 
@@ -537,7 +558,7 @@ int ofhe_hip_ntt_mul_intt(ofhe_plan_t p, const uint64_t* a_, const uint64_t* b, 
     if (!a_ || !b || !c) return fail(OFHE_ERR_ARG, "NULL data pointer");
     if (b == c && a_ != c) return fail(OFHE_ERR_ARG, "c may alias a but not b");
     HIPCHK(hipSetDevice(p->ctx->device));
-    const PlanArgs a = args_of(p);
+    const PlanArgs a = fused_args(p);
     hipStream_t s = pick(stream);
     if (p->log_n < 12) {
         launch_small<MODE_FUSED>(a, p->spq, a_, c, b, batch, s);
@@ -581,7 +602,7 @@ int ofhe_hip_ntt_mul_intt_stage(ofhe_plan_t p, int stage, const uint64_t* a_, co
     if (!a_ || !b || !c) return fail(OFHE_ERR_ARG, "NULL data pointer");
     if (stage < 0 || stage > 2) return fail(OFHE_ERR_ARG, "stage must be 0, 1 or 2");
     HIPCHK(hipSetDevice(p->ctx->device));
-    const PlanArgs a = args_of(p);
+    const PlanArgs a = fused_args(p);
     hipStream_t s = pick(stream);
     if (p->log_n < 12) {
         if (stage == 1) launch_small<MODE_FUSED>(a, p->spq, a_, c, b, batch, s);
