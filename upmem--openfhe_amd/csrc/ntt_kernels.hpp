@@ -599,7 +599,11 @@ template <bool INV, bool SPQ>
 __global__ __launch_bounds__(256, OFHE_KB_WAVES) void k_tcols(PlanArgs P, const u64* src, u64* dst, u32 batch,
                                                               u32 nwg) {
     constexpr u32 N = 1u << 16, S = 256;
-    __shared__ u64 lds[LDS_WORDS];
+    // Unpadded tile: both exchange patterns (p = tid + 256k and p = 256h + r +
+    // 16k) give every LDS lane group contiguous words, so they are bank
+    // conflict free as they stand (the p + p/16 padding made the inverse's
+    // 32-lane ds_read_b64 groups 2-way conflicted).
+    __shared__ u64 lds[4096];
     const u32 tid = threadIdx.x;
     const u32 wid = xcd_remap(blockIdx.x, nwg);
     const u32 cb = wid % (S / 16);
@@ -612,7 +616,7 @@ __global__ __launch_bounds__(256, OFHE_KB_WAVES) void k_tcols(PlanArgs P, const 
     const u64 q = tc.q;
     const Mod<SPQ> M = load_mod<SPQ>(tc);
     const u32 h = tid >> 4, r = tid & 15;
-    const u32 L1 = tid + h, L2 = h * 272 + r;
+    const u32 L1 = tid, L2 = h * 256 + r;
     u64 v[16];
     if (!INV) {
         const u64* tw = P.tw + (u64)t * N * 2;
@@ -621,11 +625,11 @@ __global__ __launch_bounds__(256, OFHE_KB_WAVES) void k_tcols(PlanArgs P, const 
         for (int k = 0; k < 16; k++) v[k] = ld_s(x + (u64)(h + 16 * k) * S + r);
         fwd_round16(v, tw, 1, M);
 #pragma unroll
-        for (int k = 0; k < 16; k++) lds[L1 + 272 * k] = v[k];
+        for (int k = 0; k < 16; k++) lds[L1 + 256 * k] = v[k];
         __syncthreads();
         // round 2: rows 16h + k (p = 256h + r + 16k), stages m = 16..128
 #pragma unroll
-        for (int k = 0; k < 16; k++) v[k] = lds[L2 + 17 * k];
+        for (int k = 0; k < 16; k++) v[k] = lds[L2 + 16 * k];
         fwd_round16(v, tw, 16 + h, M);
 #pragma unroll
         for (int k = 0; k < 16; k++) st_s(y + (u64)(16 * h + k) * S + r, v[k]);
@@ -635,10 +639,10 @@ __global__ __launch_bounds__(256, OFHE_KB_WAVES) void k_tcols(PlanArgs P, const 
         for (int k = 0; k < 16; k++) v[k] = ld_s(x + (u64)(16 * h + k) * S + r);
         inv_round16(v, itw, 16 + h, M);
 #pragma unroll
-        for (int k = 0; k < 16; k++) lds[L2 + 17 * k] = v[k];
+        for (int k = 0; k < 16; k++) lds[L2 + 16 * k] = v[k];
         __syncthreads();
 #pragma unroll
-        for (int k = 0; k < 16; k++) v[k] = lds[L1 + 272 * k];
+        for (int k = 0; k < 16; k++) v[k] = lds[L1 + 256 * k];
         inv_round16(v, itw, 1, M);
 #pragma unroll
         for (int k = 0; k < 16; k++) st_s(y + (u64)(h + 16 * k) * S + r, canon4(v[k], q));
