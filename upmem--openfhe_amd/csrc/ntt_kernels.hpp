@@ -6,21 +6,27 @@
 //   (x_j + w x_{j+t}, x_j - w x_{j+t}) with w = Table[m + i];
 //   inverse, Gentleman-Sande: m = N/2 ... 1 (t = 1 ... N/2),
 //   (x_j + x_{j+t}, (x_j - x_{j+t}) * TableI[m + i]), with n^-1 fused into the
-//   first (t = 1) stage.
-// Values stay lazily reduced between stages (forward in [0, 8q), inverse in
-// [0, 4q)) and are made canonical on output, so results equal the reference
-// bit for bit (its outputs are the canonical residues).
+//   first (t = 1) stage.  Here the inverse's first stages (those inside the
+//   block pass) run as a cyclic decimation-in-time transform plus a twist --
+//   the same values, see dit_round3() below -- and its column-pass stages as
+//   the reference's GS.
+// Values stay lazily reduced between stages (forward and DIT in [0, 16q),
+// GS in [0, 4q)) and are made canonical on output, so results equal the
+// reference bit for bit (its outputs are the canonical residues).
 //
 // Decomposition for N = 2^logN >= 2^12 (one tower = 512 KiB at 2^16, more
 // than a CU's 160 KiB LDS):
-//   k_cols  : the first logN-12 stages. Each thread owns one or two "columns"
-//             {c + 4096 k}; all its butterflies are in registers.
-//   k_block : the last 12 stages on contiguous 4096-element blocks (34 KiB of
-//             LDS per workgroup): 3 rounds of 4 radix-2 stages held in
-//             registers (16 values per thread), two padded LDS exchanges
-//             between rounds (see lds_pad()).
-//   The metric pipeline runs k_cols(fwd) -> k_block(fwd + Hadamard + inverse)
-//   -> k_cols(inv): the Hadamard and the 24 block stages share one residency.
+//   column pass: the first logN-12 stages (k_cols: each thread owns one or
+//             two "columns" {c + 4096 k}, all butterflies in registers), or at
+//             N = 2^16 the first 8 stages on 16-column x 256-row tiles
+//             (k_tcols);
+//   k_block : the last 12 (8 at N = 2^16) stages on contiguous 4096-element
+//             blocks (34 KiB of LDS per workgroup): rounds of 4 radix-2
+//             stages held in registers (16 values per thread), padded LDS
+//             exchanges between rounds (see lds_pad()).
+//   The metric pipeline runs column pass (fwd) -> k_block (fwd + Hadamard +
+//   inverse) -> column pass (inv): the Hadamard and the block stages of both
+//   directions share one residency.
 // N <= 2^11 uses k_small (whole tower in LDS, one stage per step).
 // Every kernel is instantiated for generic moduli (SPQ = false) and for
 // moduli q = 2^L - d, d < 2^32 (SPQ = true, one fewer multiply per Shoup).
