@@ -96,6 +96,8 @@ def main():
                     help="pipeline = the headline metric (configs[2]); keyswitch = configs[4] HYBRID "
                          "key switching (secondary line, not the headline)")
     ap.add_argument("--ks-batch", type=int, default=8, help="ciphertext polynomials per GPU (keyswitch)")
+    ap.add_argument("--pcie-batch", type=int, default=32, help="polynomials per chunk of the PCIe-inclusive run")
+    ap.add_argument("--pcie-chunks", type=int, default=16, help="chunks of the PCIe-inclusive run (0 = skip)")
     args = ap.parse_args()
     if args.workload == "keyswitch":
         return bench_keyswitch(args)
@@ -233,6 +235,13 @@ def main():
             ok = ok and bool(np.array_equal(cc, O.ntt_mul_intt(aa, bb, tb)))
         parity = ok
 
+    # PCIe-inclusive rate (DESIGN.md §(d)): a and b in pinned host memory, c back
+    # to host, chunks pipelined over three streams (H2D, compute, D2H).  A side
+    # figure, never `value`.
+    pcie = None
+    if rank == 0 and world == 1 and args.pcie_chunks > 0 and B >= 2 * args.pcie_batch:
+        pcie = pcie_inclusive(plan, a, b, c, args.pcie_batch, args.pcie_chunks, dev)
+
     # CPU baseline: the oracle (C, OpenMP over batch x towers) on a bounded sample
     cpu = None
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
@@ -282,6 +291,7 @@ def main():
             "pipeline_hbm_frac": value / world * ALG_BYTES_PER_COEFF / (HBM_PEAK_GBS * 1e9),
             "kernels_ms": kernels,
             "cpu_baseline": cpu,
+            "pcie_inclusive": pcie,
             "parity_spot_check": parity,
             "evalkey_broadcast": bcast,
         }
@@ -289,6 +299,52 @@ def main():
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def pcie_inclusive(plan, a, b, c, bc, chunks, dev):
+    """c = INTT(NTT(a) (.) b) with a, b in pinned host memory and c returned to
+    it: chunk i's H2D, chunk i-1's pipeline and chunk i-2's D2H overlap on three
+    streams; device slots alternate over the first 2*bc entries of a, b, c.
+    Returns coefficients/s over `chunks` chunks of `bc` polynomials."""
+    import torch
+
+    T, n = a.shape[1], a.shape[2]
+    ha, hb, hc = (torch.empty((bc, T, n), dtype=torch.int64, pin_memory=True) for _ in range(3))
+    ha.copy_(a[:bc])
+    hb.copy_(b[:bc])
+    s_in, s_run, s_out = (torch.cuda.Stream(dev) for _ in range(3))
+    ev = {k: [torch.cuda.Event() for _ in range(2)] for k in ("in", "run", "out")}
+    for k in ev:
+        for e in ev[k]:
+            e.record(torch.cuda.current_stream(dev))
+
+    def go():
+        for i in range(chunks):
+            sl = i % 2
+            da, db, dc = a[sl * bc:(sl + 1) * bc], b[sl * bc:(sl + 1) * bc], c[sl * bc:(sl + 1) * bc]
+            s_in.wait_event(ev["run"][sl])          # chunk i-2 no longer reads da, db
+            with torch.cuda.stream(s_in):
+                da.copy_(ha, non_blocking=True)
+                db.copy_(hb, non_blocking=True)
+            ev["in"][sl].record(s_in)
+            s_run.wait_event(ev["in"][sl])
+            s_run.wait_event(ev["out"][sl])         # chunk i-2's c has left the device
+            plan.ntt_mul_intt(da.data_ptr(), db.data_ptr(), dc.data_ptr(), bc, s_run.cuda_stream)
+            ev["run"][sl].record(s_run)
+            s_out.wait_event(ev["run"][sl])
+            with torch.cuda.stream(s_out):
+                hc.copy_(dc, non_blocking=True)
+            ev["out"][sl].record(s_out)
+        torch.cuda.synchronize(dev)
+
+    go()  # warm (first pinned transfers, plan tables)
+    t0 = time.perf_counter()
+    go()
+    el = time.perf_counter() - t0
+    coeffs = chunks * bc * T * n
+    return {"value": coeffs / el, "unit": "coeffs/s", "chunk_batch": bc, "chunks": chunks,
+            "pcie_bytes_per_coeff": 24, "pcie_gbs": coeffs * 24 / el / 1e9,
+            "note": "a, b pinned host -> HBM, pipeline, c -> pinned host; 3 streams, double-buffered"}
 
 
 def bench_keyswitch(args):
