@@ -601,41 +601,46 @@ __global__ __launch_bounds__(256, OFHE_KB_WAVES) void k_block(PlanArgs P, const 
 // much multiply work as HBM time, instead of k_cols' 4 stages that leave the
 // VALU idle behind HBM.
 // ---------------------------------------------------------------------------
+#ifndef OFHE_TCOLS_W
+#define OFHE_TCOLS_W 16  // tile width in columns: 16 (128-byte row segments) or 32 (256-byte)
+#endif
+constexpr u32 TCOLS_W = OFHE_TCOLS_W;
+static_assert(TCOLS_W == 16 || TCOLS_W == 32, "column tile width");
 template <bool INV, bool SPQ>
-__global__ __launch_bounds__(256, OFHE_KB_WAVES) void k_tcols(PlanArgs P, const u64* src, u64* dst, u32 batch,
-                                                              u32 nwg) {
-    constexpr u32 N = 1u << 16, S = 256;
-    // Unpadded tile: both exchange patterns (p = tid + 256k and p = 256h + r +
-    // 16k) give every LDS lane group contiguous words, so they are bank
-    // conflict free as they stand (the p + p/16 padding made the inverse's
+__global__ __launch_bounds__(16 * TCOLS_W, OFHE_KB_WAVES) void k_tcols(PlanArgs P, const u64* src, u64* dst,
+                                                                       u32 batch, u32 nwg) {
+    constexpr u32 N = 1u << 16, S = 256, W = TCOLS_W;
+    // Unpadded tile: both exchange patterns (p = tid + 16W k and p = 16W h +
+    // W k + r) give every LDS lane group contiguous words, so they are bank
+    // conflict free as they stand (a p + p/16 padding made the inverse's
     // 32-lane ds_read_b64 groups 2-way conflicted).
-    __shared__ u64 lds[4096];
+    __shared__ u64 lds[16 * 16 * W];
     const u32 tid = threadIdx.x;
     const u32 wid = xcd_remap(blockIdx.x, nwg);
-    const u32 cb = wid % (S / 16);
-    const u32 pb = wid / (S / 16);
+    const u32 cb = wid % (S / W);
+    const u32 pb = wid / (S / W);
     const u32 t = pb / batch, b = pb % batch;
-    const u64 inner = (u64)t * N + cb * 16;
+    const u64 inner = (u64)t * N + cb * W;
     const u64* x = src + (u64)b * P.sstride + inner;
     u64* y = dst + (u64)b * P.dstride + inner;
     const TowerConst tc = P.tc[t];
     const u64 q = tc.q;
     const Mod<SPQ> M = load_mod<SPQ>(tc);
-    const u32 h = tid >> 4, r = tid & 15;
-    const u32 L1 = tid, L2 = h * 256 + r;
+    const u32 h = tid / W, r = tid % W;
+    const u32 L1 = tid, L2 = h * 16 * W + r;
     u64 v[16];
     if (!INV) {
         const u64* tw = P.tw + (u64)t * N * 2;
-        // round 1: rows h + 16k (p = tid + 256k), stages m = 1..8
+        // round 1: rows h + 16k (p = tid + 16W k), stages m = 1..8
 #pragma unroll
         for (int k = 0; k < 16; k++) v[k] = ld_s(x + (u64)(h + 16 * k) * S + r);
         fwd_round16(v, tw, 1, M);
 #pragma unroll
-        for (int k = 0; k < 16; k++) lds[L1 + 256 * k] = v[k];
+        for (int k = 0; k < 16; k++) lds[L1 + 16 * W * k] = v[k];
         __syncthreads();
-        // round 2: rows 16h + k (p = 256h + r + 16k), stages m = 16..128
+        // round 2: rows 16h + k (p = 16W h + W k + r), stages m = 16..128
 #pragma unroll
-        for (int k = 0; k < 16; k++) v[k] = lds[L2 + 16 * k];
+        for (int k = 0; k < 16; k++) v[k] = lds[L2 + W * k];
         fwd_round16(v, tw, 16 + h, M);
 #pragma unroll
         for (int k = 0; k < 16; k++) st_s(y + (u64)(16 * h + k) * S + r, v[k]);
@@ -645,10 +650,10 @@ __global__ __launch_bounds__(256, OFHE_KB_WAVES) void k_tcols(PlanArgs P, const 
         for (int k = 0; k < 16; k++) v[k] = ld_s(x + (u64)(16 * h + k) * S + r);
         inv_round16(v, itw, 16 + h, M);
 #pragma unroll
-        for (int k = 0; k < 16; k++) lds[L2 + 16 * k] = v[k];
+        for (int k = 0; k < 16; k++) lds[L2 + W * k] = v[k];
         __syncthreads();
 #pragma unroll
-        for (int k = 0; k < 16; k++) v[k] = lds[L1 + 256 * k];
+        for (int k = 0; k < 16; k++) v[k] = lds[L1 + 16 * W * k];
         inv_round16(v, itw, 1, M);
 #pragma unroll
         for (int k = 0; k < 16; k++) st_s(y + (u64)(h + 16 * k) * S + r, canon4(v[k], q));

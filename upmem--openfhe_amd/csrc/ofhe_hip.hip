@@ -437,8 +437,9 @@ static void launch_block(const PlanArgs& a, bool spq, const u64* src, u64* dst, 
 }
 
 static void launch_tcols(const PlanArgs& a, bool spq, bool inv, const u64* src, u64* dst, u32 batch, hipStream_t s) {
-    const u32 nwg = batch * a.towers * 16;
-#define LT(I, SP) hipLaunchKernelGGL((k_tcols<I, SP>), dim3(nwg), dim3(256), 0, s, a, src, dst, batch, nwg)
+    const u32 nwg = batch * a.towers * (256 / TCOLS_W);
+#define LT(I, SP) \
+    hipLaunchKernelGGL((k_tcols<I, SP>), dim3(nwg), dim3(16 * TCOLS_W), 0, s, a, src, dst, batch, nwg)
     if (inv) {
         if (spq) LT(true, true); else LT(true, false);
     } else {
