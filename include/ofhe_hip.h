@@ -71,6 +71,12 @@ int ofhe_hip_free(ofhe_ctx_t ctx, void* dptr);
  * buffer can be dropped right after the asynchronous calls that use it. */
 int ofhe_hip_alloc_async(ofhe_ctx_t ctx, size_t bytes, void** dptr, void* stream);
 int ofhe_hip_free_async(ofhe_ctx_t ctx, void* dptr, void* stream);
+/* Pinned (page-locked) host memory for the staging buffers of a host-buffer
+ * integration: towers gathered from the reference's per-tower vectors
+ * (dcrtpoly.h:421, poly.h:368) into one buffer that DMA can read directly,
+ * so host <-> device copies run at the PCIe rate and overlap compute. */
+int ofhe_hip_host_alloc(ofhe_ctx_t ctx, size_t bytes, void** hptr);
+int ofhe_hip_host_free(ofhe_ctx_t ctx, void* hptr);
 /* dst[0..bytes) = 0 on the stream (a zero DCRTPoly, dcrtpoly.h initializing ctor). */
 int ofhe_hip_zero(ofhe_ctx_t ctx, void* dst, size_t bytes, void* stream);
 /* PimManager::copy_to_pim (scatter, type 0) / copy_from_pim (PimManager.h:44-54) */

@@ -385,6 +385,81 @@ int main() {
         EXPECT_THROW(X.AutomorphismTransform(4), math_error, "even index");
     });
     // error behaviour: OPENFHE_THROW analogues
+    // PlanCache: parameter objects over one basis share a plan (the reference's
+    // static per-modulus maps, transformnat.h:352-368); another basis does not.
+    TEST("PlanCache.shared_per_basis", [] {
+        const uint32_t m = 1u << 13;
+        std::vector<uint64_t> q;
+        uint64_t x = first_prime(60, m);
+        for (int t = 0; t < 3; t++) q.push_back(x = previous_prime(x, m));
+        auto A = params(m, q), B = params(m, q);
+        auto C = params(m, std::vector<uint64_t>(q.begin(), q.begin() + 2));
+        EXPECT_EQ(A->plan() == B->plan(), true, "same basis, same plan");
+        EXPECT_EQ(A->plan() == C->plan(), false, "other basis, other plan");
+    });
+    // Staging: the INTEGRATION.md host-buffer hook.  Towers live in separate
+    // host vectors (PolyImpl values); gather into pinned memory, one forward
+    // NTT over all towers, scatter back == DCRTPolyHip::SwitchFormat.
+    TEST("Staging.gather_switchformat_scatter", [] {
+        const uint32_t m = 1u << 14, n = m / 2;
+        std::vector<uint64_t> q;
+        uint64_t x = first_prime(60, m);
+        for (int t = 0; t < 4; t++) q.push_back(x = previous_prime(x, m));
+        auto P = params(m, q);
+        std::mt19937_64 rng(17);
+        std::vector<std::vector<uint64_t>> towers(4, std::vector<uint64_t>(n));
+        std::vector<uint64_t> flat;
+        for (int t = 0; t < 4; t++)
+            for (auto& v : towers[t]) flat.push_back(v = rng() % q[t]);
+        Staging st(P->manager(), (size_t)4 * n);
+        std::vector<const uint64_t*> src;
+        std::vector<uint64_t*> dst;
+        for (auto& tv : towers) src.push_back(tv.data()), dst.push_back(tv.data());
+        st.gather(src, n);
+        st.upload();
+        ofhe::check(ofhe_hip_ntt_fwd(P->plan(), st.dev(), 1, nullptr), "ntt_fwd");
+        st.download();
+        st.scatter(dst, n);
+        DCRTPolyHip ref(P, Format::COEFFICIENT);
+        ref.SetValues(flat, Format::COEFFICIENT);
+        ref.SwitchFormat();
+        auto want = ref.GetValues();
+        bool ok = true;
+        for (int t = 0; t < 4; t++)
+            for (uint32_t i = 0; i < n; i++) ok = ok && towers[t][i] == want[(size_t)t * n + i];
+        EXPECT_EQ(ok, true, "staged transform equals SwitchFormat");
+        EXPECT_THROW(st.gather(std::vector<const uint64_t*>(5, src[0]), n), math_error, "gather overflow");
+    });
+    // KsCache / KeyCache: one key-switch engine per parameter set, keys resident
+    // by id; a switch through the caches equals one through fresh objects.
+    TEST("KsCache.KeyCache.core", [] {
+        const uint32_t m = 1u << 11, n = m / 2, dnum = 2;
+        std::vector<uint64_t> all;
+        uint64_t x = first_prime(60, m);
+        for (int t = 0; t < 6; t++) all.push_back(x = previous_prime(x, m));
+        std::vector<uint64_t> q(all.begin(), all.begin() + 4), p(all.begin() + 4, all.end());
+        auto PQ = params(m, q), PP = params(m, p), PQP = params(m, all);
+        auto ks1 = KsCache::get(*PQ, *PP, dnum), ks2 = KsCache::get(*PQ, *PP, dnum);
+        EXPECT_EQ(ks1.get() == ks2.get(), true, "one engine per parameter set");
+        EXPECT_EQ(ks1.get() == KsCache::get(*PQ, *PP, 4).get(), false, "dnum is part of the key");
+        std::mt19937_64 rng(23);
+        std::vector<uint64_t> kb((size_t)dnum * 6 * n), ka(kb.size()), c((size_t)4 * n);
+        for (size_t i = 0; i < kb.size(); i++) kb[i] = rng() % all[(i / n) % 6], ka[i] = rng() % all[(i / n) % 6];
+        for (size_t i = 0; i < c.size(); i++) c[i] = rng() % q[i / n];
+        DCRTPolyHip KB(PQP, Format::EVALUATION, dnum), KA(PQP, Format::EVALUATION, dnum), C(PQ, Format::EVALUATION);
+        KB.SetValues(kb, Format::EVALUATION);
+        KA.SetValues(ka, Format::EVALUATION);
+        C.SetValues(c, Format::EVALUATION);
+        KeyCache::put("relin", DCRTPolyHip(KB), DCRTPolyHip(KA));
+        auto key = KeyCache::get("relin");
+        auto viaCache = ks1->KeySwitchCore(C, key->b, key->a);
+        KeySwitchHybrid fresh(*PQ, *PP, dnum);
+        auto direct = fresh.KeySwitchCore(C, KB, KA);
+        EXPECT_EQ(viaCache.first, direct.first, "ct0");
+        EXPECT_EQ(viaCache.second, direct.second, "ct1");
+        KeyCache::erase("relin");
+        EXPECT_THROW(KeyCache::get("relin"), math_error, "erased key");
+    });
     TEST("DCRTPolyHip.errors", [] {
         auto P = params(16, {first_prime(22, 16)});
         auto P2 = params(16, {next_prime(first_prime(22, 16), 16)});

@@ -99,6 +99,22 @@ int ofhe_hip_free_async(ofhe_ctx_t ctx, void* dptr, void* stream) {
     return OFHE_OK;
 }
 
+int ofhe_hip_host_alloc(ofhe_ctx_t ctx, size_t bytes, void** hptr) {
+    if (!ctx || !hptr) return fail(OFHE_ERR_ARG, "NULL argument");
+    HIPCHK(hipSetDevice(ctx->device));
+    hipError_t e = hipHostMalloc(hptr, bytes ? bytes : 1, hipHostMallocDefault);
+    if (e != hipSuccess) return fail(OFHE_ERR_NOMEM, std::string("hipHostMalloc: ") + hipGetErrorString(e));
+    return OFHE_OK;
+}
+
+int ofhe_hip_host_free(ofhe_ctx_t ctx, void* hptr) {
+    if (!ctx) return fail(OFHE_ERR_ARG, "ctx is NULL");
+    if (!hptr) return OFHE_OK;
+    HIPCHK(hipSetDevice(ctx->device));
+    HIPCHK(hipHostFree(hptr));
+    return OFHE_OK;
+}
+
 int ofhe_hip_zero(ofhe_ctx_t ctx, void* dst, size_t bytes, void* stream) {
     if (!ctx || (!dst && bytes)) return fail(OFHE_ERR_ARG, "NULL argument");
     if (!bytes) return OFHE_OK;

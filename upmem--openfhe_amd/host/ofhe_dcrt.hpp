@@ -10,6 +10,15 @@
 //                                dcrtpoly-impl.h:410-416, 1034-1063, 2518-2524):
 //                                SwitchFormat/SetFormat, Plus/Minus/Times and the
 //                                in-place operators, scalar Times, ApproxSwitchCRTBasis.
+//   PlanCache                 <- ChineseRemainderTransformFTTNat's static
+//                                per-modulus twiddle maps (transformnat.h:352-368)
+//   Staging                   <- the per-vector host->DPU push of PimData
+//                                (PimData.h:16-21): towers gathered from
+//                                separate host vectors into pinned memory, one
+//                                transfer each way
+//   KsCache / KeyCache        <- the per-parameter-set HYBRID tables
+//                                (rns-cryptoparameters.cpp:72-345) and the
+//                                evaluation keys kept resident on the device
 // Errors: any non-zero C-ABI status becomes ofhe::math_error, the analogue of
 // OPENFHE_THROW(math_error, ...) (src/core/include/utils/exception.h:162).
 // Device layout: a DCRTPolyHip of `batch` polynomials is one contiguous
@@ -18,6 +27,7 @@
 #pragma once
 
 #include <cstdint>
+#include <cstring>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -139,9 +149,106 @@ private:
 };
 
 // ---------------------------------------------------------------------------
-// Parameters: (cyclotomic order, moduli, roots) as ILDCRTParams, with the NTT
-// plan cached per (N, moduli) -- the reference caches twiddles per modulus in
-// static maps (transformnat.h:352-368).
+// PlanCache: one resident NTT plan per (device, N, moduli, roots), shared by
+// every DCRTParams over that basis and kept for the process lifetime, as the
+// reference's static per-modulus maps keep their tables (transformnat.h:352-368,
+// filled in PreCompute, transformnat-impl.h:708-763).
+// ---------------------------------------------------------------------------
+class PlanHandle {
+public:
+    PlanHandle(HipManager* m, uint32_t log_n, const std::vector<uint64_t>& q, const std::vector<uint64_t>& r) {
+        check(ofhe_hip_plan_create(m->ctx(), log_n, (uint32_t)q.size(), q.data(), r.data(), &p_), "PlanCache");
+    }
+    ~PlanHandle() {
+        if (p_) ofhe_hip_plan_destroy(p_);
+    }
+    PlanHandle(const PlanHandle&) = delete;
+    PlanHandle& operator=(const PlanHandle&) = delete;
+    ofhe_plan_t get() const { return p_; }
+
+private:
+    ofhe_plan_t p_ = nullptr;
+};
+
+class PlanCache {
+public:
+    static std::shared_ptr<PlanHandle> get(int device, uint32_t log_n, const std::vector<uint64_t>& moduli,
+                                           const std::vector<uint64_t>& roots) {
+        if (moduli.size() != roots.size() || moduli.empty()) throw math_error("PlanCache: moduli/roots size mismatch");
+        // the manager's statics first: destroyed after the cached plans
+        HipManager* m = HipManager::getHip(device);
+        static std::mutex mu;
+        static std::map<Key, std::shared_ptr<PlanHandle>> plans;
+        std::lock_guard<std::mutex> lk(mu);
+        auto& e = plans[Key{device, log_n, moduli, roots}];
+        if (!e) e = std::make_shared<PlanHandle>(m, log_n, moduli, roots);
+        return e;
+    }
+
+private:
+    struct Key {
+        int device;
+        uint32_t log_n;
+        std::vector<uint64_t> q, r;
+        bool operator<(const Key& o) const {
+            if (device != o.device) return device < o.device;
+            if (log_n != o.log_n) return log_n < o.log_n;
+            if (q != o.q) return q < o.q;
+            return r < o.r;
+        }
+    };
+};
+
+// ---------------------------------------------------------------------------
+// Staging: pinned host buffer + device buffer of `words` u64.  A host-buffer
+// integration gathers a DCRTPoly's towers (separate std::vectors in the
+// reference, dcrtpoly.h:421) into it, uploads once, runs one launch over all
+// towers, and scatters the result back.
+// ---------------------------------------------------------------------------
+class Staging {
+public:
+    Staging(HipManager* m, size_t words) : m_(m), dev_(m, words), n_(words) {
+        void* h = nullptr;
+        check(ofhe_hip_host_alloc(m_->ctx(), words * sizeof(uint64_t), &h), "Staging");
+        host_ = static_cast<uint64_t*>(h);
+    }
+    ~Staging() {
+        if (host_) {
+            (void)ofhe_hip_sync(m_->ctx(), nullptr);
+            (void)ofhe_hip_host_free(m_->ctx(), host_);
+        }
+    }
+    Staging(const Staging&) = delete;
+    Staging& operator=(const Staging&) = delete;
+    uint64_t* host() const { return host_; }
+    uint64_t* dev() const { return dev_.get(); }
+    size_t words() const { return n_; }
+    // towers[t] points at n words (one PolyImpl's values); they land at t*n
+    void gather(const std::vector<const uint64_t*>& towers, size_t n) {
+        if (towers.size() * n > n_) throw math_error("Staging::gather: more words than the buffer holds");
+        for (size_t t = 0; t < towers.size(); t++) std::memcpy(host_ + t * n, towers[t], n * sizeof(uint64_t));
+    }
+    void scatter(const std::vector<uint64_t*>& towers, size_t n) const {
+        if (towers.size() * n > n_) throw math_error("Staging::scatter: more words than the buffer holds");
+        for (size_t t = 0; t < towers.size(); t++) std::memcpy(towers[t], host_ + t * n, n * sizeof(uint64_t));
+    }
+    // pinned memory: DMA straight from / to the staging buffer
+    void upload() { check(ofhe_hip_copy_to_device(m_->ctx(), dev(), host_, n_ * 8, nullptr), "Staging::upload"); }
+    void download() {
+        check(ofhe_hip_copy_to_host(m_->ctx(), host_, dev(), n_ * 8, nullptr), "Staging::download");
+        m_->sync();
+    }
+
+private:
+    HipManager* m_;
+    DeviceBuffer dev_;
+    size_t n_;
+    uint64_t* host_ = nullptr;
+};
+
+// ---------------------------------------------------------------------------
+// Parameters: (cyclotomic order, moduli, roots) as ILDCRTParams; the NTT plan
+// comes from PlanCache, so parameter objects over the same basis share it.
 // ---------------------------------------------------------------------------
 class DCRTParams {
 public:
@@ -153,11 +260,7 @@ public:
         uint32_t n = m_ / 2, lg = 0;
         while ((1u << lg) < n) lg++;
         log_n_ = lg;
-        check(ofhe_hip_plan_create(mgr_->ctx(), log_n_, (uint32_t)q_.size(), q_.data(), r_.data(), &plan_),
-              "DCRTParams: plan");
-    }
-    ~DCRTParams() {
-        if (plan_) ofhe_hip_plan_destroy(plan_);
+        plan_ = PlanCache::get(device, log_n_, q_, r_);
     }
     DCRTParams(const DCRTParams&) = delete;
     DCRTParams& operator=(const DCRTParams&) = delete;
@@ -167,14 +270,14 @@ public:
     size_t Towers() const { return q_.size(); }
     const std::vector<uint64_t>& Moduli() const { return q_; }
     const std::vector<uint64_t>& Roots() const { return r_; }
-    ofhe_plan_t plan() const { return plan_; }
+    ofhe_plan_t plan() const { return plan_->get(); }
     HipManager* manager() const { return mgr_; }
 
 private:
     uint32_t m_, log_n_ = 0;
     std::vector<uint64_t> q_, r_;
     HipManager* mgr_;
-    ofhe_plan_t plan_ = nullptr;
+    std::shared_ptr<PlanHandle> plan_;
 };
 
 enum class Format { EVALUATION = 0, COEFFICIENT = 1 };
@@ -422,6 +525,60 @@ private:
     ofhe_ks_t h_ = nullptr;
     size_t sizeQ_ = 0, sizeP_ = 0;
     uint32_t numPartQ_ = 0;
+};
+
+// KsCache: one KeySwitchHybrid per (device, N, Q, P, dnum) -- the reference
+// precomputes its HYBRID CRT tables once per CryptoParametersRNS
+// (rns-cryptoparameters.cpp:72-345).
+class KsCache {
+public:
+    static std::shared_ptr<KeySwitchHybrid> get(const DCRTParams& Q, const DCRTParams& P, uint32_t numPartQ) {
+        static std::mutex mu;
+        static std::map<std::vector<uint64_t>, std::shared_ptr<KeySwitchHybrid>> cache;
+        std::vector<uint64_t> key{(uint64_t)Q.manager()->device(), Q.LogN(), numPartQ, Q.Towers()};
+        key.insert(key.end(), Q.Moduli().begin(), Q.Moduli().end());
+        key.insert(key.end(), P.Moduli().begin(), P.Moduli().end());
+        std::lock_guard<std::mutex> lk(mu);
+        auto& e = cache[key];
+        if (!e) e = std::make_shared<KeySwitchHybrid>(Q, P, numPartQ);
+        return e;
+    }
+};
+
+// KeyCache: evaluation keys resident on the device, uploaded once per key
+// (when EvalMultKeyGen / EvalAtIndexKeyGen store them) and looked up by the
+// caller's key id (e.g. the EvalKey's tag) at every key switch.
+class KeyCache {
+public:
+    struct Key {
+        DCRTPolyHip b, a;  // numPartQ polynomials over Q|P each (EvalKeyRelin's b and a vectors)
+    };
+    static std::shared_ptr<const Key> put(const std::string& id, DCRTPolyHip b, DCRTPolyHip a) {
+        auto k = std::make_shared<const Key>(Key{std::move(b), std::move(a)});
+        std::lock_guard<std::mutex> lk(mu());
+        map()[id] = k;
+        return k;
+    }
+    static std::shared_ptr<const Key> get(const std::string& id) {
+        std::lock_guard<std::mutex> lk(mu());
+        auto it = map().find(id);
+        if (it == map().end()) throw math_error("KeyCache: no evaluation key '" + id + "'");
+        return it->second;
+    }
+    static void erase(const std::string& id) {
+        std::lock_guard<std::mutex> lk(mu());
+        map().erase(id);
+    }
+
+private:
+    static std::mutex& mu() {
+        static std::mutex m;
+        return m;
+    }
+    static std::map<std::string, std::shared_ptr<const Key>>& map() {
+        static std::map<std::string, std::shared_ptr<const Key>> m;
+        return m;
+    }
 };
 
 }  // namespace ofhe

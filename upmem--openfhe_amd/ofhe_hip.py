@@ -53,6 +53,8 @@ _SIGS = {
     "ofhe_hip_free": (ctypes.c_int, [_vp, _vp]),
     "ofhe_hip_alloc_async": (ctypes.c_int, [_vp, ctypes.c_size_t, ctypes.POINTER(_vp), _vp]),
     "ofhe_hip_free_async": (ctypes.c_int, [_vp, _vp, _vp]),
+    "ofhe_hip_host_alloc": (ctypes.c_int, [_vp, ctypes.c_size_t, ctypes.POINTER(_vp)]),
+    "ofhe_hip_host_free": (ctypes.c_int, [_vp, _vp]),
     "ofhe_hip_zero": (ctypes.c_int, [_vp, _vp, ctypes.c_size_t, _vp]),
     "ofhe_hip_copy_to_device": (ctypes.c_int, [_vp, _vp, _vp, ctypes.c_size_t, _vp]),
     "ofhe_hip_copy_to_host": (ctypes.c_int, [_vp, _vp, _vp, ctypes.c_size_t, _vp]),
@@ -180,6 +182,15 @@ class Context:
 
     def free_async(self, ptr: int, stream: int = 0) -> None:
         _check(lib().ofhe_hip_free_async(self.handle, _vp(ptr), _vp(stream or None)))
+
+    def host_alloc(self, nbytes: int) -> int:
+        """Pinned host memory (staging for host-buffer integrations)."""
+        p = _vp()
+        _check(lib().ofhe_hip_host_alloc(self.handle, int(nbytes), ctypes.byref(p)))
+        return p.value
+
+    def host_free(self, ptr: int) -> None:
+        _check(lib().ofhe_hip_host_free(self.handle, _vp(ptr)))
 
     def zero(self, dst: int, nbytes: int, stream: int = 0) -> None:
         _check(lib().ofhe_hip_zero(self.handle, _vp(dst), int(nbytes), _vp(stream or None)))
