@@ -126,6 +126,53 @@ def test_approx_mod_down(hip, log_n, sq, sp, generic, t):
     assert np.array_equal(host(out), K.approx_mod_down(x, q, rq, p, rp, t))
 
 
+@pytest.mark.parametrize("sq", [1, 7, 16])
+def test_base_conversion_max_sums(hip, sq):
+    """Largest sums the limb kernel reduces: every input q_i - 1 (q_i up to
+    2^60 - 1), QHatInvModq = 1 and every QHatModp entry p_j - 1, for output
+    moduli from 2 to 2^60 - 1 (powers of two included).  Expected values by
+    Python integers: out_j = sum_i (q_i - 1)(p_j - 1) mod p_j."""
+    H, ctx = hip
+    import torch
+
+    log_n, n = 5, 32
+    q = [(1 << 60) - 1 - 2 * i for i in range(sq)]
+    p = [2, 3, 1 << 31, (1 << 32) + 15, (1 << 45) + 7, (1 << 59) + 1, (1 << 60) - 1, 1 << 59, 97]
+    bc = H.BaseConverter(ctx, log_n, q, p, [1] * sq, [pj - 1 for _ in q for pj in p])
+    rng = np.random.default_rng(sq)
+    x = np.stack([np.full(n, qi - 1, np.uint64) for qi in q])
+    x[:, 1::2] = np.stack([rng.integers(0, qi, size=n // 2, dtype=np.uint64) for qi in q])
+    dx = dev(x[None])
+    out = torch.zeros((1, len(p), n), dtype=torch.int64, device="cuda")
+    bc.switch(dx.data_ptr(), out.data_ptr(), 1, stream())
+    want = np.array([[sum(int(x[i, k]) * (pj - 1) for i in range(sq)) % pj for k in range(n)] for pj in p],
+                    np.uint64)
+    assert np.array_equal(host(out)[0], want)
+
+
+def test_keyswitch_inner_max_values(hip):
+    """Inner product with every digit and key word m - 1 (the largest limb sums
+    of the batch-stationary kernel), against the oracle."""
+    H, ctx = hip
+    import torch
+
+    n, q, rq, p, rp, kp, ks = _ks_case(H, ctx, 6, 5, 3, 2)
+    l, B = 5, 3
+    alpha, beta = ks.digits(l)
+    mods = np.array(q[:l] + p, np.uint64)[None, :, None]
+    digits = np.broadcast_to(mods - 1, (B * beta, l + len(p), n)).reshape(B, beta, l + len(p), n).copy()
+    allm = np.array(q + p, np.uint64)[None, :, None]
+    kb = np.broadcast_to(allm - 1, (2, len(q) + len(p), n)).copy()
+    ka = kb.copy()
+    ka[:, :, ::3] = 0
+    c0 = torch.empty((B, l + len(p), n), dtype=torch.int64, device="cuda")
+    c1 = torch.empty_like(c0)
+    dd, dkb, dka = dev(digits), dev(kb), dev(ka)
+    ks.fast_core_ext(l, dd.data_ptr(), dkb.data_ptr(), dka.data_ptr(), c0.data_ptr(), c1.data_ptr(), B, stream())
+    r0, r1 = K.ks_fast_core_ext(kp, digits, kb, ka)
+    assert np.array_equal(host(c0), r0) and np.array_equal(host(c1), r1)
+
+
 def _ks_case(H, ctx, log_n, sq, sp, dnum, generic=False):
     n = 1 << log_n
     q, rq, p, rp = (_generic_bases if generic else _bases)(log_n, sq, sp)
@@ -140,6 +187,8 @@ KS_CASES = [
     (12, 6, 2, 3, True),    # generic moduli
     (13, 8, 3, 3, False),   # alpha = 3, digits 3+3+2
     (16, 6, 2, 3, False),   # N = 2^16 (8|8 split transforms)
+    (5, 8, 2, 4, False),    # beta = 4 (largest batch-stationary inner product)
+    (5, 10, 2, 5, False),   # beta = 5 (generic inner product kernel)
 ]
 
 

@@ -61,6 +61,7 @@ struct BconvArgs {
     const u64* qhlimb;    // [sizeQ][sizeP rounded up to BCONV_PT], (c mod 2^30) | (c >> 30) << 32, zero padded
     const u64* pv;        // [sizeP]
     const u64* pmu;       // [sizeP][2]  (mu_lo, mu_hi) = floor(2^128 / p)
+    const u64* pred;      // [sizeP][3]  (2^60 mod p, its Shoup precon, floor(2^64 / p)): limb_reduce
     u64 in_stride;        // words between batch entries of x   (sizeQ * N when dense)
     u64 out_stride;       // words between batch entries of out (sizeP * N when dense)
     u32 log_n, size_q, size_p;
@@ -113,9 +114,8 @@ __global__ __launch_bounds__(256) void k_bconv(BconvArgs A, const u64* __restric
 //   A0 = sum y0 c0, A1 = sum y0 c1, A2 = sum y1 c0, A3 = sum y1 c1,
 // where every A is a sum of at most 16 products below 2^60: four
 // v_mad_u64_u32 per term and no carry handling (mul128 plus a 128-bit add
-// needs the same four multiplies and the carries).  The 128-bit total is
-// reduced with the same BarrettUint128ModUint64, so the output is the same
-// canonical value.  The limb table is zero-padded to a multiple of PT
+// needs the same four multiplies and the carries).  The total is reduced by
+// limb_reduce to the canonical value BarrettUint128ModUint64 gives.  The limb table is zero-padded to a multiple of PT
 // columns so the inner loop has no branches.
 // ---------------------------------------------------------------------------
 constexpr u32 LIMB = 30;
@@ -126,15 +126,38 @@ constexpr u64 LIMB_MASK = (1ull << LIMB) - 1;
 constexpr u32 BCONV_PT = OFHE_BCONV_PT;  // output towers per tile
 constexpr u32 BCONV_LIMB_QMAX = 16;
 
-__device__ __forceinline__ void limbs_to_u128(u64 a0, u64 a1, u64 a2, u64 a3, u64& lo, u64& hi) {
-    const u64 m = a1 + a2;
-    const u64 mc = m < a1;  // carry of the middle sum (weight 2^94)
-    lo = a0 + (m << LIMB);
-    u64 c = lo < a0;
-    const u64 t = a3 << (2 * LIMB);
-    lo += t;
-    c += lo < t;
-    hi = (m >> (64 - LIMB)) + (mc << LIMB) + (a3 >> (64 - 2 * LIMB)) + c;
+// S mod m for S = A0 + (A1 + A2) 2^30 + A3 2^60 < 2^124 (every limb sum below
+// 2^64; m < 2^60), canonical: the value BarrettUint128ModUint64 returns for
+// the same S, with about half its instructions.  Write S = H 2^60 + L,
+// L < 2^60 (H < 2^64 by the bound on S); then
+//   r1 = H * (2^60 mod m) mod m in [0, 4m)       (Shoup, shoup_lazy)
+//   T  = r1 + L < 4m + 2^60 < 2^63
+//   r2 = T - floor~(T * floor(2^64/m) / 2^64) m  in [0, 4m)
+// (the quotient estimate is at most 3 short: 1 from the truncated reciprocal,
+// 2 from mulhi_approx), and two conditional subtractions.  R carries
+// (m, 2^60 mod m, its Shoup precon, floor(2^64 / m)); UNI: m is wave-uniform.
+struct LimbRed {
+    u64 m, r60, r60p, mu1;
+};
+template <bool UNI>
+__device__ __forceinline__ u64 limb_reduce(u64 a0, u64 a1, u64 a2, u64 a3, const LimbRed& R) {
+    constexpr u64 M60 = (1ull << 60) - 1;
+    const u64 mid = a1 + a2;
+    const u64 mh = (mid >> LIMB) | ((u64)(mid < a1) << (64 - LIMB));  // (A1 + A2) >> 30, 65-bit sum
+    const u64 low = (a0 & M60) + ((mid & LIMB_MASK) << LIMB);          // < 2^61
+    const u64 H = a3 + mh + (a0 >> 60) + (low >> 60);
+    const Mod<false> M{R.m, 0, 0, 0 - R.m, 0, 0, 0};
+    const u64 t = shoup_lazy(H, R.r60, R.r60p, M) + (low & M60);
+    const u64 qh = mulhi_approx(t, R.mu1);
+    const u64 nq = 0 - R.m;
+    const u64 s = mad32(lo32(qh), lo32(nq), t);  // t - qh m, low 64 bits
+    u64 r = pack(lo32(s), hi32(s) + lo32(qh) * hi32(nq) + hi32(qh) * lo32(nq));
+    if (UNI) {
+        r = csub_s(r, 2 * R.m);
+        return csub_s(r, R.m);
+    }
+    r = csub(r, 2 * R.m);
+    return csub(r, R.m);
 }
 
 template <int PT>
@@ -176,10 +199,9 @@ __global__ __launch_bounds__(256) void k_bconv_limb(BconvArgs A, const u64* __re
         for (int j = 0; j < PT; j++) {
             const u32 jj = j0 + j;
             if (jj < A.size_p) {
-                u64 lo, hi;
-                limbs_to_u128(a0[j], a1[j], a2[j], a3[j], lo, hi);
                 const u32 jo = jj >= A.gap_at ? jj + A.gap : jj;
-                st_s(ob + (u64)jo * N, barrett128(lo, hi, A.pv[jj], A.pmu[2 * jj], A.pmu[2 * jj + 1]));
+                const LimbRed R{A.pv[jj], A.pred[3 * jj], A.pred[3 * jj + 1], A.pred[3 * jj + 2]};
+                st_s(ob + (u64)jo * N, limb_reduce<true>(a0[j], a1[j], a2[j], a3[j], R));
             }
         }
     }

@@ -45,6 +45,14 @@ inline u64 powmod(u64 b, u64 e, u64 q) {
 }
 inline u64 invmod(u64 a, u64 q) { return powmod(a, q - 2, q); }  // q prime
 inline u64 shoup_pre(u64 w, u64 q) { return (u64)(((u128)w << 64) / q); }
+// limb_reduce constants of a modulus m < 2^60: 2^60 mod m, its Shoup
+// precon, floor(2^64 / m)
+inline void limb_red_consts(u64 m, u64* out) {
+    const u64 r60 = (1ull << 60) % m;
+    out[0] = r60;
+    out[1] = shoup_pre(r60, m);
+    out[2] = (u64)(((u128)1 << 64) / m);
+}
 inline unsigned msb64(u64 x) { return x ? 64u - (unsigned)__builtin_clzll(x) : 0u; }
 inline u32 bitrev(u32 x, unsigned bits) {
     u32 r = 0;

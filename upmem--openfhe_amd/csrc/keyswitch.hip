@@ -212,6 +212,7 @@ struct ofhe_ks_s {
     u32 log_n = 0, size_q = 0, size_p = 0, num_part_q = 0, alpha = 0;
     std::vector<u64> q, p;
     ofhe_plan_t plan = nullptr;  // towers q[0..size_q) then p[0..size_p)
+    hipStream_t side[2] = {nullptr, nullptr};  // fork streams (OFHE_KS_STREAMS=1: none)
     std::mutex mu;
     std::map<u32, KsLevel*> levels;
 };
@@ -259,6 +260,18 @@ int ofhe_hip_ks_create(ofhe_ctx_t ctx, uint32_t log_n, uint32_t size_q, const ui
     k->q = mq;
     k->p = mp;
     k->plan = plan;
+    const char* ns = getenv("OFHE_KS_STREAMS");
+    if (!(ns && atoi(ns) == 1)) {
+        hipError_t e = hipSetDevice(ctx->device);
+        for (int i = 0; i < 2 && e == hipSuccess; i++) e = hipStreamCreateWithFlags(&k->side[i], hipStreamNonBlocking);
+        if (e != hipSuccess) {
+            for (auto& st : k->side)
+                if (st) (void)hipStreamDestroy(st);
+            ofhe_hip_plan_destroy(plan);
+            delete k;
+            return fail(OFHE_ERR_HIP, std::string("key-switch streams: ") + hipGetErrorString(e));
+        }
+    }
     *out = k;
     return OFHE_OK;
 }
@@ -268,6 +281,8 @@ int ofhe_hip_ks_destroy(ofhe_ks_t k) {
     if (k->ctx) (void)hipSetDevice(k->ctx->device);
     (void)hipDeviceSynchronize();
     for (auto& kv : k->levels) level_free(kv.second);
+    for (auto& st : k->side)
+        if (st) (void)hipStreamDestroy(st);
     if (k->plan) ofhe_hip_plan_destroy(k->plan);
     delete k;
     return OFHE_OK;
@@ -340,7 +355,9 @@ static int level_get(ofhe_ks_t k, u32 size_ql, KsLevel** out) {
             const bool isq = i < l;
             const u64 m = isq ? k->q[i] : k->p[i - l];
             const u128 mu = (~(u128)0) / m;
-            tow[i] = KsTower{m, (u64)mu, (u64)(mu >> 64), (isq ? i : k->size_q + i - l) * N};
+            u64 lr[3];
+            limb_red_consts(m, lr);
+            tow[i] = KsTower{m, (u64)mu, (u64)(mu >> 64), (isq ? i : k->size_q + i - l) * N, lr[0], lr[1], lr[2]};
         }
         std::vector<TowerScalar> pinv(l);
         for (u32 i = 0; i < l; i++)
@@ -385,6 +402,44 @@ static int level_t_tables(ofhe_ks_t k, KsLevel* L, u64 t, const TowerScalar** ou
     return OFHE_OK;
 }
 
+// Fork of the caller's stream onto the engine's two side streams, so that
+// independent digits (ModUp) and the two ModDowns overlap: each alone is a
+// sequence of short launches over a few towers that leaves the chip partly
+// idle at its head and tail.  The join (explicit, or in the destructor on an
+// error path) puts the caller's stream behind both; declare a KsFork after
+// any stream-ordered Scratch its work uses, so it joins before they are freed.
+struct KsFork {
+    hipStream_t parent = nullptr;
+    hipStream_t f[2] = {nullptr, nullptr};
+    hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
+    bool forked = false;
+    int open(ofhe_ks_t k, hipStream_t s) {
+        parent = f[0] = f[1] = s;
+        if (!k->side[0]) return OFHE_OK;
+        for (auto& e : ev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        HIPCHK(hipEventRecord(ev[0], s));
+        for (int i = 0; i < 2; i++) HIPCHK(hipStreamWaitEvent(k->side[i], ev[0], 0));
+        f[0] = k->side[0];
+        f[1] = k->side[1];
+        forked = true;
+        return OFHE_OK;
+    }
+    int join() {
+        if (!forked) return OFHE_OK;
+        forked = false;
+        for (int i = 0; i < 2; i++) {
+            HIPCHK(hipEventRecord(ev[1 + i], f[i]));
+            HIPCHK(hipStreamWaitEvent(parent, ev[1 + i], 0));
+        }
+        return OFHE_OK;
+    }
+    ~KsFork() {
+        (void)join();
+        for (auto& e : ev)
+            if (e) (void)hipEventDestroy(e);
+    }
+};
+
 static int ks_check(ofhe_ks_t k, u32 size_ql, u32 batch) {
     if (!k || !k->ctx) return fail(OFHE_ERR_STATE, "key switch is NULL or destroyed");
     if (size_ql < 1 || size_ql > k->size_q) return fail(OFHE_ERR_ARG, "size_ql must be in [1, size_q]");
@@ -399,10 +454,12 @@ int ofhe_hip_ks_precompute(ofhe_ks_t k, uint32_t size_ql, const uint64_t* c, uin
     if (!c || !digits) return fail(OFHE_ERR_ARG, "NULL data pointer");
     KsLevel* L = nullptr;
     RCCHK(level_get(k, size_ql, &L));
-    hipStream_t s = pick(stream);
+    KsFork fk;
+    RCCHK(fk.open(k, pick(stream)));
     const u64 N = 1ull << k->log_n, l = size_ql, P = k->size_p, poly = (l + P) * N, ds = L->beta * poly;
     for (u32 j = 0; j < L->beta; j++) {
         const u32 st = L->start[j], n = L->cnt[j];
+        hipStream_t s = fk.f[j & 1];  // digits are independent
         u64* slot = digits + j * poly;
         // partsCt[j] in coefficient form (keyswitch-hybrid.cpp:384-385)
         RCCHK(plan_ntt_range(k->plan, true, st, n, c + st * N, slot + st * N, l * N, ds, batch, s));
@@ -420,7 +477,7 @@ int ofhe_hip_ks_precompute(ofhe_ks_t k, uint32_t size_ql, const uint64_t* c, uin
         // the digit's own towers stay as given (evaluation form, 402-404)
         RCCHK(copy_rows(slot + st * N, ds, c + st * N, l * N, (u64)n * N, batch, s));
     }
-    return OFHE_OK;
+    return fk.join();
 }
 
 int ofhe_hip_ks_fast_core_ext(ofhe_ks_t k, uint32_t size_ql, const uint64_t* digits, const uint64_t* key_b,
@@ -432,11 +489,20 @@ int ofhe_hip_ks_fast_core_ext(ofhe_ks_t k, uint32_t size_ql, const uint64_t* dig
     const u32 towers = size_ql + k->size_p;
     const u64 key_stride = (u64)(k->size_q + k->size_p) << k->log_n;
     if (L->beta <= 4) {
-        // batch-stationary keys: one thread per (tower, coefficient pair)
-        const u64 rows = ((u64)towers << k->log_n) / 2;
-        const u64 blocks = (rows + 255) / 256;
-        hipLaunchKernelGGL(k_ks_inner_bs<4>, dim3((u32)blocks), dim3(256), 0, pick(stream), L->d_tow, digits, key_b,
-                           key_a, ct0, ct1, key_stride, L->beta, batch, rows, k->log_n, towers);
+        // batch-stationary keys: one thread per (tower, OFHE_KS_CPT coefficients)
+        const u64 rows = ((u64)towers << k->log_n) / OFHE_KS_CPT;
+        const dim3 g((u32)((rows + 255) / 256)), blk(256);
+        hipStream_t s = pick(stream);
+#define OFHE_KS_BS(B_)                                                                                      \
+    hipLaunchKernelGGL((k_ks_inner_bs<B_, OFHE_KS_CPT>), g, blk, 0, s, L->d_tow, digits, key_b, key_a, ct0, ct1, \
+                       key_stride, batch, rows, k->log_n, towers)
+        switch (L->beta) {
+            case 1: OFHE_KS_BS(1); break;
+            case 2: OFHE_KS_BS(2); break;
+            case 3: OFHE_KS_BS(3); break;
+            default: OFHE_KS_BS(4); break;
+        }
+#undef OFHE_KS_BS
     } else {
         const u64 npairs = ((u64)batch * towers << k->log_n) / 2;
         hipLaunchKernelGGL(k_ks_inner, dim3(grid_for(npairs)), dim3(256), 0, pick(stream), L->d_tow, digits, key_b,
@@ -479,8 +545,11 @@ int ofhe_hip_ks_core(ofhe_ks_t k, uint32_t size_ql, const uint64_t* c, const uin
     u64* c1 = ct.w() + (u64)batch * poly;
     RCCHK(ofhe_hip_ks_precompute(k, size_ql, c, dg.w(), batch, s));
     RCCHK(ofhe_hip_ks_fast_core_ext(k, size_ql, dg.w(), key_b, key_a, c0, c1, batch, s));
-    RCCHK(ks_mod_down_impl(k, L, c0, out0, t, batch, s));
-    return ks_mod_down_impl(k, L, c1, out1, t, batch, s);
+    KsFork fk;  // after dg, ct: joins before they are freed
+    RCCHK(fk.open(k, s));
+    RCCHK(ks_mod_down_impl(k, L, c0, out0, t, batch, fk.f[0]));
+    RCCHK(ks_mod_down_impl(k, L, c1, out1, t, batch, fk.f[1]));
+    return fk.join();
 }
 
 // ---------------------------------------------------------------------------

@@ -63,9 +63,10 @@ __global__ __launch_bounds__(256) void k_sub_scale(const TowerScalar* __restrict
 
 // Tower of the extended basis Ql|P for the key-switch inner product.
 struct KsTower {
-    u64 m;             // modulus
-    u64 mu_lo, mu_hi;  // floor(2^128 / m)
-    u64 key_off;       // word offset of this tower inside one key polynomial (QP layout)
+    u64 m;                // modulus
+    u64 mu_lo, mu_hi;     // floor(2^128 / m)
+    u64 key_off;          // word offset of this tower inside one key polynomial (QP layout)
+    u64 r60, r60p, mu1;   // limb_reduce constants
 };
 
 // EvalFastKeySwitchCoreExt (keyswitch-hybrid.cpp:452-478):
@@ -113,72 +114,103 @@ __global__ __launch_bounds__(256) void k_ks_inner(const KsTower* __restrict__ tw
     }
 }
 
-// Same product, batch-stationary keys: a thread owns (tower, coefficient
-// pair) and walks the batch, so each key word is read once per launch instead
-// of once per ciphertext.  Sums use the 30-bit limb split of k_bconv_limb
-// (beta <= 16 terms below 2^60 per limb sum).  Digits j >= beta are masked by
-// zero key limbs, keeping the loop branch-free.
-template <int BMAX>
+// Same product, batch-stationary keys: a thread owns (tower, C coefficients)
+// and walks the batch, so each key word is read once per launch instead of
+// once per ciphertext.  Sums use the 30-bit limb split and limb_reduce of
+// k_bconv_limb (beta <= 16 terms below 2^60 per limb sum).  BETA is the exact
+// digit count (no masked slots), and the next ciphertext's digits are loaded
+// before the current one is reduced, so one load latency hides behind a
+// whole iteration of arithmetic.  C = 1 halves the per-thread state of C = 2
+// (more waves in flight: the kernel is latency- rather than issue-bound).
+#ifndef OFHE_KS_CPT
+#define OFHE_KS_CPT 1
+#endif
+template <int C>
+struct Words {
+    u64 v[C];
+};
+template <int C>
+__device__ __forceinline__ Words<C> ldw(const u64* p) {
+    Words<C> w;
+    if constexpr (C == 2) {
+        const u64x2 t = ld2_s(p);
+        w.v[0] = t.x;
+        w.v[1] = t.y;
+    } else {
+        w.v[0] = ld_s(p);
+    }
+    return w;
+}
+template <int C>
+__device__ __forceinline__ void stw(u64* p, const u64* v) {
+    if constexpr (C == 2) {
+        u64x2 t;
+        t.x = v[0];
+        t.y = v[1];
+        st2_s(p, t);
+    } else {
+        st_s(p, v[0]);
+    }
+}
+
+template <int BETA, int C>
 __global__ __launch_bounds__(256) void k_ks_inner_bs(const KsTower* __restrict__ tw, const u64* __restrict__ digits,
                                                      const u64* __restrict__ kb, const u64* __restrict__ ka,
                                                      u64* __restrict__ ct0, u64* __restrict__ ct1, u64 key_stride,
-                                                     u32 beta, u32 batch, u64 npairs_row, u32 log_n, u32 towers) {
+                                                     u32 batch, u64 nthreads, u32 log_n, u32 towers) {
     const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= npairs_row) return;
-    const u64 e = 2 * i;
+    if (i >= nthreads) return;
+    const u64 e = C * i;
     const u32 t = (u32)(e >> log_n), c = (u32)(e & ((1ull << log_n) - 1));
     const KsTower T = tw[t];
+    const LimbRed R{T.m, T.r60, T.r60p, T.mu1};
     const u64 poly = (u64)towers << log_n;
     const u64 inner = ((u64)t << log_n) + c;
-    u64 kl[BMAX][4];  // (b.x, b.y, a.x, a.y) as (lo30 | hi30 << 32)
+    u64 kl[BETA][2 * C];  // (b[0..C), a[0..C)) as (lo30 | hi30 << 32)
 #pragma unroll
-    for (int j = 0; j < BMAX; j++) {
-        const bool on = j < (int)beta;
-        const u64 off = T.key_off + c + (u64)(on ? j : 0) * key_stride;
-        const u64x2 vb = ld2_s(kb + off);
-        const u64x2 va = ld2_s(ka + off);
-        const u64 w[4] = {vb.x, vb.y, va.x, va.y};
+    for (int j = 0; j < BETA; j++) {
+        const u64 off = T.key_off + c + (u64)j * key_stride;
+        const Words<C> vb = ldw<C>(kb + off), va = ldw<C>(ka + off);
 #pragma unroll
-        for (int k = 0; k < 4; k++) kl[j][k] = on ? ((w[k] & LIMB_MASK) | ((w[k] >> LIMB) << 32)) : 0;
+        for (int k = 0; k < C; k++) {
+            kl[j][k] = (vb.v[k] & LIMB_MASK) | ((vb.v[k] >> LIMB) << 32);
+            kl[j][C + k] = (va.v[k] & LIMB_MASK) | ((va.v[k] >> LIMB) << 32);
+        }
     }
-#ifndef OFHE_KS_UNROLL
-#define OFHE_KS_UNROLL 1
-#endif
-#pragma unroll OFHE_KS_UNROLL
+    Words<C> xn[BETA];
+#pragma unroll
+    for (int j = 0; j < BETA; j++) xn[j] = ldw<C>(digits + (u64)j * poly + inner);
     for (u32 b = 0; b < batch; b++) {
-        const u64* d = digits + (u64)b * beta * poly + inner;
-        u64 acc[4][4];
+        Words<C> x[BETA];
 #pragma unroll
-        for (int k = 0; k < 4; k++) acc[k][0] = acc[k][1] = acc[k][2] = acc[k][3] = 0;
+        for (int j = 0; j < BETA; j++) x[j] = xn[j];
+        if (b + 1 < batch) {
+            const u64* d = digits + (u64)(b + 1) * BETA * poly + inner;
 #pragma unroll
-        for (int j = 0; j < BMAX; j++) {
-            const u64x2 x = ld2_s(d + (u64)(j < (int)beta ? j : 0) * poly);
-            const u32 x0[2] = {(u32)(x.x & LIMB_MASK), (u32)(x.y & LIMB_MASK)};
-            const u32 x1[2] = {(u32)(x.x >> LIMB), (u32)(x.y >> LIMB)};
+            for (int j = 0; j < BETA; j++) xn[j] = ldw<C>(d + (u64)j * poly);
+        }
+        u64 acc[2 * C][4];  // k < C: ct0 coefficient k; k >= C: ct1 coefficient k - C
 #pragma unroll
-            for (int k = 0; k < 4; k++) {  // k: (ct0, coef 0), (ct0, 1), (ct1, 0), (ct1, 1)
+        for (int k = 0; k < 2 * C; k++) acc[k][0] = acc[k][1] = acc[k][2] = acc[k][3] = 0;
+#pragma unroll
+        for (int j = 0; j < BETA; j++) {
+#pragma unroll
+            for (int k = 0; k < 2 * C; k++) {
+                const u64 xv = x[j].v[k % C];
+                const u32 x0 = (u32)(xv & LIMB_MASK), x1 = (u32)(xv >> LIMB);
                 const u64 kw = kl[j][k];
-                acc[k][0] = mad32(x0[k & 1], lo32(kw), acc[k][0]);
-                acc[k][1] = mad32(x0[k & 1], hi32(kw), acc[k][1]);
-                acc[k][2] = mad32(x1[k & 1], lo32(kw), acc[k][2]);
-                acc[k][3] = mad32(x1[k & 1], hi32(kw), acc[k][3]);
+                acc[k][0] = mad32(x0, lo32(kw), acc[k][0]);
+                acc[k][1] = mad32(x0, hi32(kw), acc[k][1]);
+                acc[k][2] = mad32(x1, lo32(kw), acc[k][2]);
+                acc[k][3] = mad32(x1, hi32(kw), acc[k][3]);
             }
         }
-        u64 r[4];
+        u64 r[2 * C];
 #pragma unroll
-        for (int k = 0; k < 4; k++) {
-            u64 lo, hi;
-            limbs_to_u128(acc[k][0], acc[k][1], acc[k][2], acc[k][3], lo, hi);
-            r[k] = barrett128(lo, hi, T.m, T.mu_lo, T.mu_hi);
-        }
+        for (int k = 0; k < 2 * C; k++) r[k] = limb_reduce<false>(acc[k][0], acc[k][1], acc[k][2], acc[k][3], R);
         const u64 o = (u64)b * poly + inner;
-        u64x2 w0, w1;
-        w0.x = r[0];
-        w0.y = r[1];
-        w1.x = r[2];
-        w1.y = r[3];
-        st2_s(ct0 + o, w0);
-        st2_s(ct1 + o, w1);
+        stw<C>(ct0 + o, r);
+        stw<C>(ct1 + o, r + C);
     }
 }
 

@@ -689,6 +689,11 @@ int ofhe_hip_modmul_scalar(ofhe_plan_t p, const uint64_t* a, const uint64_t* s, 
 // ---------------------------------------------------------------------------
 // Base conversion
 // ---------------------------------------------------------------------------
+namespace {
+template <class T>
+T* pred_of(T* qhlimb, u32 qrows, u32 ppad) { return qhlimb + (size_t)qrows * ppad; }
+}  // namespace
+
 int ofhe_hip_bconv_create(ofhe_ctx_t ctx, uint32_t log_n, uint32_t size_q, uint32_t size_p,
                           const uint64_t* q, const uint64_t* p, const uint64_t* qhat_inv_modq,
                           const uint64_t* qhat_modp, ofhe_bconv_t* out) {
@@ -700,10 +705,11 @@ int ofhe_hip_bconv_create(ofhe_ctx_t ctx, uint32_t log_n, uint32_t size_q, uint3
         if (q[i] < 2 || q[i] >= (1ull << 60)) return fail(OFHE_ERR_ARG, "q out of range");
     for (u32 j = 0; j < size_p; j++)
         if (p[j] < 2 || p[j] >= (1ull << 60)) return fail(OFHE_ERR_ARG, "p out of range");
-    // layout: qv[Q] | qhinv[2Q] | qhmodp[Q*P] | pv[P] | pmu[2P] | qhlimb[Q*Ppad]
+    // layout: qv[Q] | qhinv[2Q] | qhmodp[Q*P] | pv[P] | pmu[2P] | qhlimb[Q*Ppad] | pred[3P]
     const u32 ppad = (size_p + BCONV_PT - 1) / BCONV_PT * BCONV_PT;
     const u32 qrows = size_q;
-    const size_t words = size_q + 2 * size_q + (size_t)size_q * size_p + size_p + 2 * size_p + (size_t)qrows * ppad;
+    const size_t words =
+        size_q + 2 * size_q + (size_t)size_q * size_p + size_p + 2 * size_p + (size_t)qrows * ppad + 3 * size_p;
     std::vector<u64> h(words);
     u64* qv = h.data();
     u64* qhinv = qv + size_q;
@@ -727,6 +733,7 @@ int ofhe_hip_bconv_create(ofhe_ctx_t ctx, uint32_t log_n, uint32_t size_q, uint3
         const u128 mu = (~(u128)0) / p[j];  // floor(2^128 / p), p odd
         pmu[2 * j] = (u64)mu;
         pmu[2 * j + 1] = (u64)(mu >> 64);
+        limb_red_consts(p[j], pred_of(qhlimb, qrows, ppad) + 3 * j);
     }
     ofhe_bconv_s* b = new (std::nothrow) ofhe_bconv_s();
     if (!b) return fail(OFHE_ERR_NOMEM, "bconv allocation failed");
@@ -746,6 +753,7 @@ int ofhe_hip_bconv_create(ofhe_ctx_t ctx, uint32_t log_n, uint32_t size_q, uint3
     A.pv = A.qhmodp + (size_t)size_q * size_p;
     A.pmu = A.pv + size_p;
     A.qhlimb = A.pmu + 2 * size_p;
+    A.pred = pred_of(A.qhlimb, qrows, ppad);
     A.log_n = log_n;
     A.size_q = size_q;
     A.size_p = size_p;
