@@ -146,12 +146,14 @@ def main():
         key = torch.empty(shard.evalkey_words(T, log_n, 3), dtype=torch.int64, device=dev)
         if rank == 0:
             key.random_(0, qs[-1], generator=g)
+        bfn, backend = shard.key_broadcaster(ctx, rank, world)
         dist.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        shard.broadcast_evalkey(key, src=0)
+        bfn(key, 0)
         torch.cuda.synchronize()
-        bcast = {"bytes": key.numel() * 8, "ms": (time.perf_counter() - t0) * 1e3, "backend": "nccl(RCCL)"}
+        bcast = {"bytes": key.numel() * 8, "ms": (time.perf_counter() - t0) * 1e3, "backend": backend,
+                 "verified": shard.same_on_all_ranks(key)}
         del key
 
     def step():
@@ -388,9 +390,12 @@ def bench_keyswitch(args):
     if rank == 0 or world == 1:
         kb.copy_(uniform((dnum, sq + sp, n), q + p))
         ka.copy_(uniform((dnum, sq + sp, n), q + p))
+    key_bcast = None
     if world > 1:  # the evaluation key comes from rank 0 over RCCL (configs[3]/[4])
-        shard.broadcast_evalkey(kb, src=0)
-        shard.broadcast_evalkey(ka, src=0)
+        bfn, backend = shard.key_broadcaster(ctx, rank, world)
+        bfn(kb, 0)
+        bfn(ka, 0)
+        key_bcast = {"backend": backend, "verified": shard.same_on_all_ranks(kb) and shard.same_on_all_ranks(ka)}
     o0 = torch.empty((B, sq, n), dtype=torch.int64, device=dev)
     o1 = torch.empty_like(o0)
     digits = torch.empty((B, beta, sq + sp, n), dtype=torch.int64, device=dev)
@@ -452,6 +457,7 @@ def bench_keyswitch(args):
                        "parallelism": f"ciphertext-batch-sharded x{world}, key broadcast over RCCL"},
             "stages_ms": stages,
             "alg_hbm_gbs": alg_words * 8 * n * B / (elapsed / args.steps) / 1e9,
+            "evalkey_broadcast": key_bcast,
         }
         print(json.dumps(out), flush=True)
     if world > 1:

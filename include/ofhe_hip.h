@@ -237,6 +237,25 @@ int ofhe_hip_switch_modulus(ofhe_ctx_t ctx, const uint64_t* src, uint64_t* dst, 
 int ofhe_hip_automorphism(ofhe_plan_t plan, uint32_t k, int eval_form, const uint64_t* src, uint64_t* dst,
                           uint32_t batch, void* stream);
 
+/* ---- multi-GPU: evaluation-key broadcast over RCCL (xGMI) ----
+ * the path shards by ciphertext batch with no exchange;
+ * the one collective is the broadcast of the key-switching keys from a root
+ * GPU (the keys the HYBRID core reads, keyswitch-hybrid.cpp:452-478).  The
+ * reference is single-device (PimManager.h:21-127 drives one DPU set), so
+ * this has no reference counterpart beyond "the key is in device memory".
+ * One communicator per (process, device); the 128-byte id from rank 0's
+ * ofhe_hip_comm_unique_id travels to the other ranks out of band. */
+#define OFHE_COMM_ID_BYTES 128
+typedef struct ofhe_comm_s* ofhe_comm_t;
+int ofhe_hip_comm_unique_id(void* id /* OFHE_COMM_ID_BYTES */);
+/* Collective over all nranks processes (blocks until they have all joined). */
+int ofhe_hip_comm_init(ofhe_ctx_t ctx, int nranks, int rank, const void* id, ofhe_comm_t* out);
+int ofhe_hip_comm_destroy(ofhe_comm_t comm);
+/* In-place broadcast of `words` u64 of device memory from rank `root`:
+ * the root's key is read, every other rank's buffer is overwritten.  Enqueued
+ * on `stream` (ncclBroadcast); all ranks must call it with the same words. */
+int ofhe_hip_bcast_evalkey(ofhe_comm_t comm, uint64_t* key, size_t words, int root, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -77,6 +77,10 @@ def test_argument_errors_without_device():
         L.ofhe_hip_bconv_create(null, 4, 1, 1, q, q, q, q, ctypes.byref(vp())),
         L.ofhe_hip_plan_destroy(null),
         L.ofhe_hip_ks_destroy(null),
+        L.ofhe_hip_comm_unique_id(null),
+        L.ofhe_hip_comm_init(null, 2, 0, null, ctypes.byref(vp())),
+        L.ofhe_hip_comm_destroy(null),
+        L.ofhe_hip_bcast_evalkey(null, null, 8, 0, null),
     ]
     assert all(rc != 0 for rc in cases), cases
     assert L.ofhe_hip_last_error()  # a message is set

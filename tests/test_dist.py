@@ -75,6 +75,8 @@ def _work(rank, world, port, q):
         shard.broadcast_evalkey(key, src=0)
         ref = torch.zeros_like(key).random_(0, 2**40, generator=torch.Generator().manual_seed(9))
         ok_bcast = bool(torch.equal(key, ref))
+        # the bench's cross-rank check of a broadcast key
+        ok_bcast = ok_bcast and shard.same_on_all_ranks(key) and not shard.same_on_all_ranks(key + rank)
         slowest = shard.max_over_ranks(float(rank + 1))
         q.put((rank, ok_pipeline, ok_bcast, slowest))
     finally:

@@ -1,0 +1,89 @@
+// comm.hip -- multi-GPU evaluation-key broadcast over RCCL (xGMI).
+//
+// the only collective of the path is a broadcast of the
+// key-switching keys from a root GPU, once per key, before any ciphertext is
+// switched; the polynomial work itself is sharded by ciphertext batch with no
+// exchange.  The reference has no multi-device path (its PimManager drives
+// one DPU set per process, PimManager.h:21-127); this is the MI355X
+// equivalent of loading the key into every device's memory.
+//
+// One communicator per (process, device): ranks exchange the 128-byte
+// unique id out of band (the caller's launcher: torch.distributed, MPI, a
+// file), then each calls ofhe_hip_comm_init.  ncclBroadcast runs in place on
+// the caller's stream, so a broadcast orders with the caller's kernels like
+// every other entry point; nothing here synchronises.
+#include <rccl/rccl.h>
+
+#include <cstring>
+#include <new>
+#include <string>
+
+#include "internal.hpp"
+
+static_assert(OFHE_COMM_ID_BYTES == NCCL_UNIQUE_ID_BYTES, "unique id size");
+
+struct ofhe_comm_s {
+    ofhe_ctx_t ctx = nullptr;
+    ncclComm_t comm = nullptr;
+    int nranks = 0, rank = 0;
+};
+
+namespace {
+int rccl_fail(const char* what, ncclResult_t r) {
+    return ofhe::fail(OFHE_ERR_HIP, std::string(what) + ": " + ncclGetErrorString(r));
+}
+}  // namespace
+
+int ofhe_hip_comm_unique_id(void* id) {
+    if (!id) return ofhe::fail(OFHE_ERR_ARG, "unique id buffer is NULL");
+    ncclUniqueId u;
+    const ncclResult_t r = ncclGetUniqueId(&u);
+    if (r != ncclSuccess) return rccl_fail("ncclGetUniqueId", r);
+    std::memcpy(id, u.internal, sizeof(u.internal));
+    return OFHE_OK;
+}
+
+int ofhe_hip_comm_init(ofhe_ctx_t ctx, int nranks, int rank, const void* id, ofhe_comm_t* out) {
+    if (!ctx || !id || !out) return ofhe::fail(OFHE_ERR_ARG, "NULL argument");
+    if (!ctx->live.load()) return ofhe::fail(OFHE_ERR_STATE, "context was finalized");
+    if (nranks < 1 || rank < 0 || rank >= nranks) return ofhe::fail(OFHE_ERR_ARG, "rank must be in [0, nranks)");
+    HIPCHK(hipSetDevice(ctx->device));
+    ncclUniqueId u;
+    std::memcpy(u.internal, id, sizeof(u.internal));
+    ncclComm_t c = nullptr;
+    const ncclResult_t r = ncclCommInitRank(&c, nranks, u, rank);
+    if (r != ncclSuccess) return rccl_fail("ncclCommInitRank", r);
+    ofhe_comm_s* s = new (std::nothrow) ofhe_comm_s();
+    if (!s) {
+        (void)ncclCommDestroy(c);
+        return ofhe::fail(OFHE_ERR_NOMEM, "communicator allocation failed");
+    }
+    s->ctx = ctx;
+    s->comm = c;
+    s->nranks = nranks;
+    s->rank = rank;
+    *out = s;
+    return OFHE_OK;
+}
+
+int ofhe_hip_comm_destroy(ofhe_comm_t c) {
+    if (!c) return ofhe::fail(OFHE_ERR_ARG, "communicator is NULL");
+    (void)hipSetDevice(c->ctx->device);
+    const ncclResult_t r = c->comm ? ncclCommDestroy(c->comm) : ncclSuccess;
+    delete c;
+    if (r != ncclSuccess) return rccl_fail("ncclCommDestroy", r);
+    return OFHE_OK;
+}
+
+int ofhe_hip_bcast_evalkey(ofhe_comm_t c, uint64_t* key, size_t words, int root, void* stream) {
+    if (!c || !c->comm) return ofhe::fail(OFHE_ERR_STATE, "communicator is NULL or destroyed");
+    if (root < 0 || root >= c->nranks) return ofhe::fail(OFHE_ERR_ARG, "root must be in [0, nranks)");
+    if (words == 0) return OFHE_OK;
+    if (!key) return ofhe::fail(OFHE_ERR_ARG, "key is NULL");
+    HIPCHK(hipSetDevice(c->ctx->device));
+    // u64 words as ncclUint64: in place (sendbuff == recvbuff), the root's
+    // buffer is read, every other rank's is overwritten
+    const ncclResult_t r = ncclBroadcast(key, key, words, ncclUint64, root, c->comm, ofhe::pick(stream));
+    if (r != ncclSuccess) return rccl_fail("ncclBroadcast", r);
+    return OFHE_OK;
+}

@@ -99,7 +99,13 @@ _SIGS = {
     "ofhe_hip_switch_modulus": (ctypes.c_int, [_vp, _vp, _vp, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64,
                                                _vp]),
     "ofhe_hip_automorphism": (ctypes.c_int, [_vp, ctypes.c_uint32, ctypes.c_int, _vp, _vp, ctypes.c_uint32, _vp]),
+    "ofhe_hip_comm_unique_id": (ctypes.c_int, [_vp]),
+    "ofhe_hip_comm_init": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int, _vp, ctypes.POINTER(_vp)]),
+    "ofhe_hip_comm_destroy": (ctypes.c_int, [_vp]),
+    "ofhe_hip_bcast_evalkey": (ctypes.c_int, [_vp, _vp, ctypes.c_size_t, ctypes.c_int, _vp]),
 }
+
+COMM_ID_BYTES = 128  # OFHE_COMM_ID_BYTES
 
 EXPORTED_SYMBOLS = tuple(_SIGS)
 
@@ -409,3 +415,41 @@ class KeySwitch:
              batch: int = 1, stream: int = 0) -> None:
         _check(lib().ofhe_hip_ks_core(self._h, int(size_ql), _vp(c), _vp(key_b), _vp(key_a), _vp(out0),
                                       _vp(out1), int(t), int(batch), _vp(stream or None)))
+
+
+def comm_unique_id() -> bytes:
+    """Rank 0's RCCL unique id (OFHE_COMM_ID_BYTES), to be sent to the others."""
+    buf = ctypes.create_string_buffer(COMM_ID_BYTES)
+    _check(lib().ofhe_hip_comm_unique_id(buf))
+    return buf.raw
+
+
+class Comm:
+    """RCCL communicator of this process's device (ofhe_hip_comm_init).
+    Collective: every rank constructs it with the same id."""
+
+    def __init__(self, ctx: Context, nranks: int, rank: int, uid: bytes):
+        if len(uid) != COMM_ID_BYTES:
+            raise MathError(f"unique id must be {COMM_ID_BYTES} bytes")
+        h = _vp()
+        buf = ctypes.create_string_buffer(bytes(uid), COMM_ID_BYTES)
+        _check(lib().ofhe_hip_comm_init(ctx.handle, int(nranks), int(rank), buf, ctypes.byref(h)))
+        self._h, self._ctx, self.nranks, self.rank = h, ctx, nranks, rank
+
+    def bcast_evalkey(self, key_ptr: int, words: int, root: int = 0, stream: int = 0) -> None:
+        """In-place broadcast of `words` u64 of device memory from `root`."""
+        if self._h is None:
+            raise MathError("communicator destroyed")
+        _check(lib().ofhe_hip_bcast_evalkey(self._h, _vp(key_ptr or None), int(words), int(root),
+                                            _vp(stream or None)))
+
+    def close(self) -> None:
+        if self._h is not None:
+            _check(lib().ofhe_hip_comm_destroy(self._h))
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -2,8 +2,10 @@
 
 The pipeline is independent per (batch, tower), so ranks shard the batch with no
 data-path collective.  The only exchange the north star names is the
-evaluation-key broadcast, done with torch.distributed (backend "nccl" is RCCL
-over xGMI on ROCm; "gloo" in CPU tests).
+evaluation-key broadcast: through the library's own RCCL communicator
+(ofhe_hip_comm_init / ofhe_hip_bcast_evalkey, open_comm + bcast_evalkey_capi
+below), or with torch.distributed (backend "nccl" is RCCL over xGMI on ROCm;
+"gloo" in CPU tests).
 """
 from __future__ import annotations
 
@@ -37,6 +39,52 @@ def broadcast_evalkey(key, src: int = 0, group=None):
 
     dist.broadcast(key, src=src, group=group)
     return key
+
+
+def open_comm(ctx, rank: int, world: int):
+    """The C ABI's RCCL communicator for this rank's device; rank 0's unique id
+    travels over the default torch.distributed group.  Collective."""
+    import torch.distributed as dist
+
+    import ofhe_hip as H
+
+    uid = [H.comm_unique_id() if rank == 0 else None]
+    dist.broadcast_object_list(uid, src=0)
+    return H.Comm(ctx, world, rank, uid[0])
+
+
+def bcast_evalkey_capi(comm, key, src: int = 0):
+    """In-place key broadcast through ofhe_hip_bcast_evalkey on the tensor's
+    current stream (key: contiguous int64/uint64 device tensor)."""
+    import torch
+
+    assert key.is_contiguous() and key.element_size() == 8
+    comm.bcast_evalkey(key.data_ptr(), key.numel(), src, torch.cuda.current_stream(key.device).cuda_stream)
+    return key
+
+
+def same_on_all_ranks(t) -> bool:
+    """True when a tensor's word checksum agrees across ranks (broadcast check)."""
+    import torch
+    import torch.distributed as dist
+
+    h = torch.stack([t.sum(), (t * 3).bitwise_xor(t >> 7).sum()]).to(torch.int64)
+    lo, hi = h.clone(), h.clone()
+    dist.all_reduce(lo, op=dist.ReduceOp.MIN)
+    dist.all_reduce(hi, op=dist.ReduceOp.MAX)
+    return bool(torch.equal(lo, hi))
+
+
+def key_broadcaster(ctx, rank: int, world: int):
+    """(broadcast function, backend label): the C-ABI communicator when it
+    comes up, else torch.distributed's own RCCL group (the failure is named)."""
+    import ofhe_hip as H
+
+    try:
+        comm = open_comm(ctx, rank, world)
+    except H.MathError as e:
+        return (lambda key, src=0: broadcast_evalkey(key, src)), f"torch.distributed nccl (C-ABI comm: {e})"
+    return (lambda key, src=0: bcast_evalkey_capi(comm, key, src)), "ofhe_hip_bcast_evalkey (RCCL)"
 
 
 def max_over_ranks(value: float, device=None) -> float:
