@@ -95,6 +95,9 @@ def main():
     ap.add_argument("--workload", default="pipeline", choices=["pipeline", "keyswitch"],
                     help="pipeline = the headline metric (configs[2]); keyswitch = configs[4] HYBRID "
                          "key switching (secondary line, not the headline)")
+    ap.add_argument("--shard", default="batch", choices=["batch", "towers"],
+                    help="batch = every rank runs its own batch of --batch (weak scaling, the default line); "
+                         "towers = configs[3]: --towers split across ranks, same batch on each (strong scaling)")
     ap.add_argument("--ks-batch", type=int, default=8, help="ciphertext polynomials per GPU (keyswitch)")
     ap.add_argument("--pcie-batch", type=int, default=32, help="polynomials per chunk of the PCIe-inclusive run")
     ap.add_argument("--pcie-chunks", type=int, default=16, help="chunks of the PCIe-inclusive run (0 = skip)")
@@ -117,14 +120,22 @@ def main():
     import ofhe_hip as H
     import shard
 
-    # weak scaling: every rank owns a batch shard of the same size
-    _, B_rank = shard.shard_batch(args.batch * world, rank, world)
-    assert B_rank == args.batch
+    log_n, T_total, B = args.log_n, args.towers, args.batch
+    if args.shard == "batch":
+        # weak scaling: every rank owns a batch shard of the same size
+        _, B_rank = shard.shard_batch(args.batch * world, rank, world)
+        assert B_rank == args.batch
+        t_start, T = 0, T_total
+    else:
+        # strong scaling (configs[3]): a contiguous tower range per rank
+        t_start, T = shard.shard_towers(T_total, rank, world)
+        if T == 0:
+            raise SystemExit(f"--shard towers needs at least one tower per rank ({T_total} over {world})")
 
     ctx = H.Context(local)
-    log_n, T, B = args.log_n, args.towers, args.batch
     n = 1 << log_n
-    qs, roots = moduli_chain(log_n, T)
+    qs_all, roots_all = moduli_chain(log_n, T_total)
+    qs, roots = qs_all[t_start:t_start + T], roots_all[t_start:t_start + T]
     plan = H.NTTPlan(ctx, log_n, qs, roots)
 
     # synthetic inputs, uniform residues mod q_t, generated on the device
@@ -143,7 +154,7 @@ def main():
     # outside the timed loop -- the only collective the path has)
     bcast = None
     if world > 1:
-        key = torch.empty(shard.evalkey_words(T, log_n, 3), dtype=torch.int64, device=dev)
+        key = torch.empty(shard.evalkey_words(T_total, log_n, 3), dtype=torch.int64, device=dev)
         if rank == 0:
             key.random_(0, qs[-1], generator=g)
         bfn, backend = shard.key_broadcaster(ctx, rank, world)
@@ -174,7 +185,7 @@ def main():
     elapsed = time.perf_counter() - t0
     if world > 1:
         elapsed = shard.max_over_ranks(elapsed, device=dev)
-    coeffs_per_step = B * T * n * world
+    coeffs_per_step = B * T * n * world if args.shard == "batch" else B * T_total * n
     value = coeffs_per_step * args.steps / elapsed
     ms_per_step = elapsed / args.steps * 1e3
 
@@ -278,14 +289,19 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": ms_per_step,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "weak" if args.shard == "batch" else "strong",
             "vs_baseline": None,
             "dtype": "u64",
             "data": "synthetic: uniform residues mod q_t (torch random_ on device), a coeff form, b eval form",
-            "config": {"workload": f"configs[2]: N=2^{log_n}, towers={T}, batch={B} per GPU, "
-                                   "c = INTT(NTT(a) (.) b)",
-                       "log_n": log_n, "towers": T, "batch_per_gpu": B, "global_batch": B * world,
-                       "parallelism": f"batch-sharded x{world} (no data-path collective)"},
+            "config": ({"workload": f"configs[2]: N=2^{log_n}, towers={T}, batch={B} per GPU, "
+                                    "c = INTT(NTT(a) (.) b)",
+                        "log_n": log_n, "towers": T, "batch_per_gpu": B, "global_batch": B * world,
+                        "parallelism": f"batch-sharded x{world} (no data-path collective)"}
+                       if args.shard == "batch" else
+                       {"workload": f"configs[3]: N=2^{log_n}, towers={T_total} split over {world} GPUs, "
+                                    f"batch={B}, c = INTT(NTT(a) (.) b)",
+                        "log_n": log_n, "towers": T_total, "towers_rank0": T, "global_batch": B,
+                        "parallelism": f"tower-sharded x{world} (no data-path collective)"}),
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": dominant,
                          "kernel_ms": kms, "alg_bytes_per_launch": ALG_BYTES_PER_COEFF * coeffs_rank,
