@@ -182,6 +182,12 @@ __global__ __launch_bounds__(256) void k_bconv_limb(BconvArgs A, const u64* __re
         u64 a0[PT], a1[PT], a2[PT], a3[PT];
 #pragma unroll
         for (int j = 0; j < PT; j++) a0[j] = a1[j] = a2[j] = a3[j] = 0;
+        // unrolled so that one s_waitcnt covers several towers' constant loads
+        // (scalar loads return out of order: each wait is lgkmcnt(0))
+#ifndef OFHE_BCONV_UNROLL
+#define OFHE_BCONV_UNROLL 4
+#endif
+#pragma unroll OFHE_BCONV_UNROLL
         for (u32 i = 0; i < A.size_q; i++) {
             const u64 yy = ys[i][tid];
             const u32 y0 = lo32(yy), y1 = hi32(yy);
