@@ -164,10 +164,12 @@ def test_random_shapes_vs_oracle(hip, O, log_n, towers, batch):
     assert np.array_equal(got["pipeline"], O.ntt_mul_intt(a, b, tb))
 
 
-def test_edge_values(hip, O):
-    """All-zero, all-(q-1) and alternating extreme inputs (lazy-reduction corners)."""
+@pytest.mark.parametrize("log_n", [14, 16, 17])
+def test_edge_values(hip, O, log_n):
+    """All-zero, all-(q-1) and alternating extreme inputs (lazy-reduction corners);
+    2^16 runs the k_tcols column pass, 2^17 k_cols (k_tcols9: test_split9_n17_vs_oracle)."""
     H, ctx = hip
-    log_n, T = 14, 3
+    T = 3 if log_n == 14 else 1
     n = 1 << log_n
     qs, rs = O.moduli_chain(log_n, T)
     tb = O.Tables(n, qs, rs)
@@ -326,6 +328,36 @@ def test_special_prime_switch_identical(hip, O, monkeypatch):
         outs.append(host(xc))
     assert np.array_equal(outs[0], outs[1])
     assert np.array_equal(outs[0], O.ntt_mul_intt(a, b, O.Tables(n, qs, rs)))
+
+
+@pytest.mark.parametrize("edge", [False, True])
+def test_split9_n17_vs_oracle(hip, O, monkeypatch, edge):
+    """N = 2^17 under OFHE_SPLIT9 (k_tcols9: 9 column stages + the 8-stage
+    block pass) gives the oracle's forward, inverse and pipeline outputs; edge
+    = all-(q-1) inputs (lazy-reduction corners of the extra stage)."""
+    import torch
+
+    H, ctx = hip
+    log_n, T, B = 17, 2, 2
+    n = 1 << log_n
+    qs, rs = O.moduli_chain(log_n, T)
+    tb = O.Tables(n, qs, rs)
+    if edge:
+        a = np.broadcast_to(np.array(qs, np.uint64)[None, :, None] - np.uint64(1), (B, T, n)).copy()
+    else:
+        a = O.uniform_dcrt(B, T, n, qs, 17)
+    b = O.uniform_dcrt(B, T, n, qs, 18)
+    monkeypatch.setenv("OFHE_SPLIT9", "1")
+    plan = H.NTTPlan(ctx, log_n, qs, rs)
+    xa, xb = dev(a), dev(b)
+    xc = torch.empty_like(xa)
+    plan.ntt_mul_intt(xa.data_ptr(), xb.data_ptr(), xc.data_ptr(), B, stream())
+    xf, xi = dev(a), dev(a)
+    plan.forward(xf.data_ptr(), B, stream())
+    plan.inverse(xi.data_ptr(), B, stream())
+    assert np.array_equal(host(xf), O.ntt_fwd(a, tb))
+    assert np.array_equal(host(xi), O.ntt_inv(a, tb))
+    assert np.array_equal(host(xc), O.ntt_mul_intt(a, b, tb))
 
 
 def test_split4_identical(hip, O, monkeypatch):

@@ -1,7 +1,7 @@
 """A/B timing of compile-time variants (upmem--openfhe_amd/lib/variants/*.so)
 on the configs[4] key switch (N = 2^17, Q = 48, P = 16, dnum = 3), in ONE
 process, interleaved rounds; checks every variant's output equals the first's.
-Env: EXP_KS_BATCH (default 8), EXP_ROUNDS (default 5), EXP_ONLY."""
+Env: EXP_KS_BATCH (default 8), EXP_ROUNDS (default 5), EXP_ONLY, EXP_TOGGLE."""
 import ctypes
 import glob
 import os
@@ -48,11 +48,20 @@ for p in paths:
     for name, (res, args) in ofhe_hip._SIGS.items():
         if hasattr(L, name):
             getattr(L, name).restype, getattr(L, name).argtypes = res, args
-    ctx, ks = vp(), vp()
+    ctx = vp()
     assert L.ofhe_hip_init(0, ctypes.byref(ctx)) == 0
-    assert L.ofhe_hip_ks_create(ctx, log_n, sq, arr(allq[:sq]), arr(allr[:sq]), sp, arr(allq[sq:]), arr(allr[sq:]),
-                                dnum, ctypes.byref(ks)) == 0, L.ofhe_hip_last_error()
-    libs.append((os.path.basename(p), L, ks))
+    # EXP_TOGGLE=VAR: a second engine per library built with VAR=1 (plan-creation
+    # switches such as OFHE_SPLIT4), timed in the same interleaved rounds
+    toggle = os.environ.get("EXP_TOGGLE")
+    for tv in ([None, toggle] if toggle else [None]):
+        if tv:
+            os.environ[tv] = "1"
+        ks = vp()
+        assert L.ofhe_hip_ks_create(ctx, log_n, sq, arr(allq[:sq]), arr(allr[:sq]), sp, arr(allq[sq:]),
+                                    arr(allr[sq:]), dnum, ctypes.byref(ks)) == 0, L.ofhe_hip_last_error()
+        if tv:
+            del os.environ[tv]
+        libs.append((os.path.basename(p) + (f"+{tv}" if tv else ""), L, ks))
 s = torch.cuda.current_stream()
 spt = vp(s.cuda_stream)
 times = {nm: [] for nm, _, _ in libs}

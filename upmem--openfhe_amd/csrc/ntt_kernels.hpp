@@ -661,6 +661,102 @@ __global__ __launch_bounds__(16 * TCOLS_W, OFHE_KB_WAVES) void k_tcols(PlanArgs 
 }
 
 // ---------------------------------------------------------------------------
+// k_tcols9: the first 9 forward stages (or the last 9 inverse stages) of an
+// N = 2^17 transform, so that the block pass keeps its 8 stages (k_block
+// NR = 2) and the two passes split the multiply work 9 | 8 instead of k_cols'
+// 5 | 12 (whose column pass sits idle behind HBM while the 12-stage block
+// pass is VALU-bound).  Element j = row * 256 + col, 512 rows.  A workgroup of
+// 512 threads owns 16 columns x 512 rows; half hf = tid / 256 holds rows
+// [256 hf, 256 hf + 256) in k_tcols' layout.  Forward: stage m = 1 pairs row
+// rho with rho + 256 (twiddle Table[1]) through one LDS exchange -- the half
+// holding y computes w y, so no product is computed twice -- then each half
+// runs k_tcols' two radix-16 rounds as the independent sub-transform it now
+// is (twiddle bases 2 + hf and 32 + 16 hf + h: index m + rho / (512 / m)).
+// Inverse: the mirror, ending in the GS stage across the halves.  Lazy bounds
+// as k_tcols: the extra forward stage maps [0, q) to [0, 5q).
+// ---------------------------------------------------------------------------
+template <bool INV, bool SPQ>
+__global__ __launch_bounds__(512) void k_tcols9(PlanArgs P, const u64* src, u64* dst, u32 batch, u32 nwg) {
+    constexpr u32 N = 1u << 17, S = 256, W = 16, HALF = 16 * 16 * W;  // words per half tile
+    __shared__ u64 lds[2 * HALF];
+    const u32 tid = threadIdx.x;
+    const u32 hf = tid >> 8, tl = tid & 255;
+    const u32 wid = xcd_remap(blockIdx.x, nwg);
+    const u32 cb = wid % (S / W);
+    const u32 pb = wid / (S / W);
+    const u32 t = pb / batch, b = pb % batch;
+    const u64 inner = (u64)t * N + (u64)hf * 256 * S + cb * W;  // row 256 hf of this tile
+    const u64* x = src + (u64)b * P.sstride + inner;
+    u64* y = dst + (u64)b * P.dstride + inner;
+    const TowerConst tc = P.tc[t];
+    const u64 q = tc.q;
+    const Mod<SPQ> M = load_mod<SPQ>(tc);
+    const u32 h = tl / W, r = tl % W;
+    u64* my = lds + hf * HALF;
+    const u64* other = lds + (hf ^ 1) * HALF;
+    const u32 L1 = tl, L2 = h * 16 * W + r;
+    u64 v[16];
+    if (!INV) {
+        const u64* tw = P.tw + (u64)t * N * 2;
+#pragma unroll
+        for (int k = 0; k < 16; k++) v[k] = ld_s(x + (u64)(h + 16 * k) * S + r);
+        // stage m = 1: (x, y) = rows (rho, rho + 256) -> (x + w y, x + 4q - w y)
+        const Tw w1 = ldtw(tw, 1);
+        if (hf) {
+#pragma unroll
+            for (int k = 0; k < 16; k++) v[k] = shoup_lazy(v[k], w1.w, w1.wp, M);  // w y, [0, 4q)
+        }
+#pragma unroll
+        for (int k = 0; k < 16; k++) my[L1 + 16 * W * k] = v[k];
+        __syncthreads();
+        if (hf) {
+#pragma unroll
+            for (int k = 0; k < 16; k++) v[k] = other[L1 + 16 * W * k] + M.q4 - v[k];
+        } else {
+#pragma unroll
+            for (int k = 0; k < 16; k++) v[k] += other[L1 + 16 * W * k];
+        }
+        __syncthreads();  // the partner has read this half's slots
+        fwd_round16(v, tw, 2 + hf, M);
+#pragma unroll
+        for (int k = 0; k < 16; k++) my[L1 + 16 * W * k] = v[k];
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < 16; k++) v[k] = my[L2 + W * k];
+        fwd_round16(v, tw, 32 + 16 * hf + h, M);
+#pragma unroll
+        for (int k = 0; k < 16; k++) st_s(y + (u64)(16 * h + k) * S + r, v[k]);
+    } else {
+        const u64* itw = P.itw + (u64)t * N * 2;
+#pragma unroll
+        for (int k = 0; k < 16; k++) v[k] = ld_s(x + (u64)(16 * h + k) * S + r);
+        inv_round16(v, itw, 32 + 16 * hf + h, M);
+#pragma unroll
+        for (int k = 0; k < 16; k++) my[L2 + W * k] = v[k];
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < 16; k++) v[k] = my[L1 + 16 * W * k];
+        inv_round16(v, itw, 2 + hf, M);
+        // each thread rewrites only the round-1 slots it read itself
+#pragma unroll
+        for (int k = 0; k < 16; k++) my[L1 + 16 * W * k] = v[k];
+        __syncthreads();
+        // stage m = 1 (GS): rows (rho, rho + 256) -> (x + y, (x - y) w), inputs [0, 4q)
+        if (hf) {
+            const Tw w1 = ldtw(itw, 1);
+#pragma unroll
+            for (int k = 0; k < 16; k++)
+                v[k] = canon4(shoup_lazy(other[L1 + 16 * W * k] + M.q4 - v[k], w1.w, w1.wp, M), q);
+        } else {
+#pragma unroll
+            for (int k = 0; k < 16; k++) v[k] = canon4(csub_s(v[k] + other[L1 + 16 * W * k], M.q4), q);
+        }
+#pragma unroll
+        for (int k = 0; k < 16; k++) st_s(y + (u64)(h + 16 * k) * S + r, v[k]);
+    }
+}
+
+// ---------------------------------------------------------------------------
 // k_cols: the first KA = logN - 12 forward stages (or the last KA inverse
 // stages) on columns {c + 4096 k}, k < 2^KA, entirely in registers.  CPT
 // adjacent columns per thread make every global access 8*CPT bytes wide.

@@ -187,7 +187,12 @@ int ofhe_hip_plan_create(ofhe_ctx_t ctx, uint32_t log_n, uint32_t towers, const 
     // DIT inverse (ntt_kernels.hpp): dtw[t + k] = psi^(-k N / t) for t = 1..N/2,
     // k < t; the block pass's output twist, and twist_r = twist * 2^64 mod q
     std::vector<u64> dtw(2 * TN), twist(2 * TN), twist_r(2 * TN);
-    const bool split8 = log_n == 16 && !getenv("OFHE_SPLIT4");
+    // 8-stage block pass (k_block NR = 2) with an 8-stage column pass at
+    // N = 2^16 (k_tcols; OFHE_SPLIT4 restores k_cols + NR = 3).  At N = 2^17
+    // the 9 | 8 split (k_tcols9) is opt-in, OFHE_SPLIT9: measured 4 % slower in
+    // key switching than k_cols (5 stages) + NR = 3 (rejected variants)
+    const bool split8 =
+        (log_n == 16 && !getenv("OFHE_SPLIT4")) || (log_n == 17 && getenv("OFHE_SPLIT9") != nullptr);
     // PreCompute (transformnat-impl.h:708-763), one host thread per tower group
     auto build = [&](u32 t) {
         const u64 qt = q[t], ps = psi[t], psinv = invmod(ps, qt);
@@ -432,12 +437,13 @@ static void launch_cols(const PlanArgs& a, bool spq, bool inv, const u64* src, u
         launch_cols_s<false>(a, inv, src, dst, batch, s);
 }
 
-// column pass for log_n > 12: k_tcols (8 stages) under split8, else k_cols
+// column pass for log_n > 12: k_tcols / k_tcols9 (8 / 9 stages) under split8, else k_cols
 static void launch_colpass(const PlanArgs& a, bool spq, bool split8, bool inv, const u64* src, u64* dst, u32 batch,
                            hipStream_t s);
 
-// Pass split for log_n > 12: with split8 (log_n == 16) the column pass does 8
-// stages (k_tcols) and the block pass the last 8 (k_block NR=2); otherwise the
+// Pass split for log_n > 12: with split8 (log_n == 16, 17) the column pass does
+// 8 (k_tcols) or 9 (k_tcols9) stages and the block pass the last 8 (k_block
+// NR=2); otherwise the
 // column pass does log_n - 12 stages in registers (k_cols) and the block pass 12.
 template <int MODE>
 static void launch_block(const PlanArgs& a, bool spq, const u64* src, u64* dst, const u64* b, u32 batch,
@@ -453,6 +459,17 @@ static void launch_block(const PlanArgs& a, bool spq, const u64* src, u64* dst, 
 }
 
 static void launch_tcols(const PlanArgs& a, bool spq, bool inv, const u64* src, u64* dst, u32 batch, hipStream_t s) {
+    if (a.log_n == 17) {
+        const u32 nwg = batch * a.towers * 16;  // 16-column tiles of 512 rows
+#define LT9(I, SP) hipLaunchKernelGGL((k_tcols9<I, SP>), dim3(nwg), dim3(512), 0, s, a, src, dst, batch, nwg)
+        if (inv) {
+            if (spq) LT9(true, true); else LT9(true, false);
+        } else {
+            if (spq) LT9(false, true); else LT9(false, false);
+        }
+#undef LT9
+        return;
+    }
     const u32 nwg = batch * a.towers * (256 / TCOLS_W);
 #define LT(I, SP) \
     hipLaunchKernelGGL((k_tcols<I, SP>), dim3(nwg), dim3(16 * TCOLS_W), 0, s, a, src, dst, batch, nwg)
