@@ -152,12 +152,12 @@ def main():
 
     # RCCL broadcast of a synthetic hybrid key-switching key (configs[3]; setup,
     # outside the timed loop -- the only collective the path has)
-    bcast = None
+    bcast, comm = None, None
     if world > 1:
         key = torch.empty(shard.evalkey_words(T_total, log_n, 3), dtype=torch.int64, device=dev)
         if rank == 0:
             key.random_(0, qs[-1], generator=g)
-        bfn, backend = shard.key_broadcaster(ctx, rank, world)
+        bfn, backend, comm = shard.key_broadcaster(ctx, rank, world)
         dist.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
@@ -315,6 +315,9 @@ def main():
         }
         print(json.dumps(out), flush=True)
     if world > 1:
+        torch.cuda.synchronize()
+        if comm is not None:
+            comm.close()
         dist.barrier()
         dist.destroy_process_group()
 
@@ -406,9 +409,9 @@ def bench_keyswitch(args):
     if rank == 0 or world == 1:
         kb.copy_(uniform((dnum, sq + sp, n), q + p))
         ka.copy_(uniform((dnum, sq + sp, n), q + p))
-    key_bcast = None
+    key_bcast, comm = None, None
     if world > 1:  # the evaluation key comes from rank 0 over RCCL (configs[3]/[4])
-        bfn, backend = shard.key_broadcaster(ctx, rank, world)
+        bfn, backend, comm = shard.key_broadcaster(ctx, rank, world)
         bfn(kb, 0)
         bfn(ka, 0)
         key_bcast = {"backend": backend, "verified": shard.same_on_all_ranks(kb) and shard.same_on_all_ranks(ka)}
@@ -477,6 +480,9 @@ def bench_keyswitch(args):
         }
         print(json.dumps(out), flush=True)
     if world > 1:
+        torch.cuda.synchronize()
+        if comm is not None:
+            comm.close()
         dist.barrier()
         dist.destroy_process_group()
 

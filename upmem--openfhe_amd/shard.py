@@ -76,15 +76,17 @@ def same_on_all_ranks(t) -> bool:
 
 
 def key_broadcaster(ctx, rank: int, world: int):
-    """(broadcast function, backend label): the C-ABI communicator when it
-    comes up, else torch.distributed's own RCCL group (the failure is named)."""
+    """(broadcast function, backend label, communicator or None): the C-ABI
+    communicator when it comes up, else torch.distributed's own RCCL group
+    (the failure is named).  Close the communicator (comm.close()) before
+    destroying the process group, not at interpreter exit."""
     import ofhe_hip as H
 
     try:
         comm = open_comm(ctx, rank, world)
     except H.MathError as e:
-        return (lambda key, src=0: broadcast_evalkey(key, src)), f"torch.distributed nccl (C-ABI comm: {e})"
-    return (lambda key, src=0: bcast_evalkey_capi(comm, key, src)), "ofhe_hip_bcast_evalkey (RCCL)"
+        return (lambda key, src=0: broadcast_evalkey(key, src)), f"torch.distributed nccl (C-ABI comm: {e})", None
+    return (lambda key, src=0: bcast_evalkey_capi(comm, key, src)), "ofhe_hip_bcast_evalkey (RCCL)", comm
 
 
 def max_over_ranks(value: float, device=None) -> float:
