@@ -121,7 +121,9 @@ __global__ __launch_bounds__(256) void k_ks_inner(const KsTower* __restrict__ tw
 // digit count (no masked slots), and the next ciphertext's digits are loaded
 // before the current one is reduced, so one load latency hides behind a
 // whole iteration of arithmetic.  C = 1 halves the per-thread state of C = 2
-// (more waves in flight: the kernel is latency- rather than issue-bound).
+// (more waves in flight).  SQ counters (configs[4]): 149 VALU instructions per
+// ciphertext per thread, two thirds of them limb_reduce, at ~66 % of the VALU
+// issue peak; a two-deep prefetch (6 loads in flight) measured no gain.
 #ifndef OFHE_KS_CPT
 #define OFHE_KS_CPT 1
 #endif
@@ -177,18 +179,8 @@ __global__ __launch_bounds__(256) void k_ks_inner_bs(const KsTower* __restrict__
             kl[j][C + k] = (va.v[k] & LIMB_MASK) | ((va.v[k] >> LIMB) << 32);
         }
     }
-    Words<C> xn[BETA];
-#pragma unroll
-    for (int j = 0; j < BETA; j++) xn[j] = ldw<C>(digits + (u64)j * poly + inner);
-    for (u32 b = 0; b < batch; b++) {
-        Words<C> x[BETA];
-#pragma unroll
-        for (int j = 0; j < BETA; j++) x[j] = xn[j];
-        if (b + 1 < batch) {
-            const u64* d = digits + (u64)(b + 1) * BETA * poly + inner;
-#pragma unroll
-            for (int j = 0; j < BETA; j++) xn[j] = ldw<C>(d + (u64)j * poly);
-        }
+    // one ciphertext: BETA digit words -> ct0/ct1 words of batch entry b
+    auto one = [&](const Words<C> (&x)[BETA], u32 b) {
         u64 acc[2 * C][4];  // k < C: ct0 coefficient k; k >= C: ct1 coefficient k - C
 #pragma unroll
         for (int k = 0; k < 2 * C; k++) acc[k][0] = acc[k][1] = acc[k][2] = acc[k][3] = 0;
@@ -211,6 +203,20 @@ __global__ __launch_bounds__(256) void k_ks_inner_bs(const KsTower* __restrict__
         const u64 o = (u64)b * poly + inner;
         stw<C>(ct0 + o, r);
         stw<C>(ct1 + o, r + C);
+    };
+    auto load = [&](Words<C> (&x)[BETA], u32 b) {
+        const u64* d = digits + (u64)b * BETA * poly + inner;
+#pragma unroll
+        for (int j = 0; j < BETA; j++) x[j] = ldw<C>(d + (u64)j * poly);
+    };
+    Words<C> xn[BETA];
+    load(xn, 0);
+    for (u32 b = 0; b < batch; b++) {
+        Words<C> x[BETA];
+#pragma unroll
+        for (int j = 0; j < BETA; j++) x[j] = xn[j];
+        if (b + 1 < batch) load(xn, b + 1);
+        one(x, b);
     }
 }
 
