@@ -7,7 +7,7 @@ mkdir -p "$R/gpurun_out/pmc"
 cd /tmp && export TMPDIR=/tmp
 for C in FETCH_SIZE WRITE_SIZE; do
   timeout -k 10 ${PMC_TIMEOUT:-300} rocprofv3 --pmc $C --kernel-trace --output-format csv \
-      -d "$R/gpurun_out/pmc/$C" -o run -- python3 "$R/bench.py" --steps 2 --warmup 1 --cpu-seconds 0 --no-check \
+      -d "$R/gpurun_out/pmc/$C" -o run -- python3 "$R/bench.py" --steps 2 --warmup 1 --cpu-seconds 0 --no-check --pcie-chunks 0 \
       ${PMC_ARGS} > "$R/gpurun_out/pmc/$C.stdout" 2> "$R/gpurun_out/pmc/$C.err" || { echo "pmc $C failed rc=$?"; exit 1; }
   echo "pmc $C done"
 done
