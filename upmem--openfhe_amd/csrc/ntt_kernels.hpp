@@ -313,6 +313,45 @@ __device__ __forceinline__ void inv_stage16(u64 (&v)[16], const u64* itw, u32 M0
     }
 }
 
+// Lazy GS radix-16 round for the inverse column pass (OFHE_LAZY_GS).  The
+// bound of every register is known at compile time (b8[k]: < 8q, else < 4q):
+// a GS butterfly's sum output is < 8q and its Shoup output < 4q whatever the
+// inputs, so only butterflies with an 8q input take the conditional subtract
+// (12 of 32 in a round fed with < 4q, 20 of 32 fed with < 8q) and the rest
+// add straight through.  d = x + Bq - y < 16q <= 2^64 (q < 2^60).
+#ifndef OFHE_LAZY_GS
+#define OFHE_LAZY_GS 1
+#endif
+template <class M_>
+__device__ __forceinline__ void gs_bfly_b(u64& x, u64& y, Tw w, const M_& M, bool in8) {
+    const u64 s = x + y;
+    const u64 d = x + (in8 ? M.q8 : M.q4) - y;
+    x = in8 ? csub_s(s, M.q8) : s;
+    y = shoup_lazy(d, w.w, w.wp, M);
+}
+template <int S, class M_>
+__device__ __forceinline__ void inv_stage16_b(u64 (&v)[16], bool (&b8)[16], const u64* itw, u32 M0, const M_& M) {
+    constexpr int half = 8 >> S;
+    const u64* base = itw + 2 * ((u64)M0 << S);
+#pragma unroll
+    for (int j = 0; j < (1 << S); j++) {
+        Tw w = ldtw(base, j);
+#pragma unroll
+        for (int k = j * 2 * half; k < j * 2 * half + half; k++) {
+            gs_bfly_b(v[k], v[k + half], w, M, b8[k] || b8[k + half]);
+            b8[k] = true;
+            b8[k + half] = false;
+        }
+    }
+}
+template <class M_>
+__device__ __forceinline__ void inv_round16_b(u64 (&v)[16], bool (&b8)[16], const u64* itw, u32 M0, const M_& M) {
+    inv_stage16_b<3>(v, b8, itw, M0, M);
+    inv_stage16_b<2>(v, b8, itw, M0, M);
+    inv_stage16_b<1>(v, b8, itw, M0, M);
+    inv_stage16_b<0>(v, b8, itw, M0, M);
+}
+
 template <class M_>
 __device__ __forceinline__ void fwd_round16(u64 (&v)[16], const u64* tw, u32 M0, const M_& M) {
     fwd_stage16<0>(v, tw, M0, M);
@@ -648,15 +687,36 @@ __global__ __launch_bounds__(16 * TCOLS_W, OFHE_KB_WAVES) void k_tcols(PlanArgs 
         const u64* itw = P.itw + (u64)t * N * 2;
 #pragma unroll
         for (int k = 0; k < 16; k++) v[k] = ld_s(x + (u64)(16 * h + k) * S + r);
-        inv_round16(v, itw, 16 + h, M);
+        if (OFHE_LAZY_GS) {
+            // input < 4q (the block pass's lazy twist); round 2's registers all
+            // come from one round-1 position, taken as < 8q
+            bool b8[16];
 #pragma unroll
-        for (int k = 0; k < 16; k++) lds[L2 + W * k] = v[k];
-        __syncthreads();
+            for (int k = 0; k < 16; k++) b8[k] = false;
+            inv_round16_b(v, b8, itw, 16 + h, M);
 #pragma unroll
-        for (int k = 0; k < 16; k++) v[k] = lds[L1 + 16 * W * k];
-        inv_round16(v, itw, 1, M);
+            for (int k = 0; k < 16; k++) lds[L2 + W * k] = v[k];
+            __syncthreads();
 #pragma unroll
-        for (int k = 0; k < 16; k++) st_s(y + (u64)(h + 16 * k) * S + r, canon4(v[k], q));
+            for (int k = 0; k < 16; k++) {
+                v[k] = lds[L1 + 16 * W * k];
+                b8[k] = true;
+            }
+            inv_round16_b(v, b8, itw, 1, M);
+#pragma unroll
+            for (int k = 0; k < 16; k++)
+                st_s(y + (u64)(h + 16 * k) * S + r, b8[k] ? canon8(v[k], q) : canon4(v[k], q));
+        } else {
+            inv_round16(v, itw, 16 + h, M);
+#pragma unroll
+            for (int k = 0; k < 16; k++) lds[L2 + W * k] = v[k];
+            __syncthreads();
+#pragma unroll
+            for (int k = 0; k < 16; k++) v[k] = lds[L1 + 16 * W * k];
+            inv_round16(v, itw, 1, M);
+#pragma unroll
+            for (int k = 0; k < 16; k++) st_s(y + (u64)(h + 16 * k) * S + r, canon4(v[k], q));
+        }
     }
 }
 
