@@ -11,7 +11,8 @@
 //   the same values, see dit_round3() below -- and its column-pass stages as
 //   the reference's GS.
 // Values stay lazily reduced between stages (forward and DIT in [0, 16q),
-// GS in [0, 4q)) and are made canonical on output, so results equal the
+// GS in [0, 8q) with compile-time bounds per register, OFHE_LAZY_GS) and are
+// made canonical on output, so results equal the
 // reference bit for bit (its outputs are the canonical residues).
 //
 // Decomposition for N = 2^logN >= 2^12 (one tower = 512 KiB at 2^16, more
@@ -853,6 +854,29 @@ __device__ __forceinline__ void cols_inv(u64 (&v)[CPT][E], const u64* itw, const
         }
     }
 }
+// lazy form (OFHE_LAZY_GS): compile-time bounds b8 as in inv_stage16_b, inputs < 4q
+template <int E, int CPT, class M_>
+__device__ __forceinline__ void cols_inv_b(u64 (&v)[CPT][E], bool (&b8)[E], const u64* itw, const M_& M) {
+    constexpr int KA = __builtin_ctz(E);
+#pragma unroll
+    for (int k = 0; k < E; k++) b8[k] = false;
+#pragma unroll
+    for (int s = KA - 1; s >= 0; s--) {
+        const int half = E >> (s + 1);
+#pragma unroll
+        for (int j = 0; j < (1 << s); j++) {
+            Tw w = ldtw(itw, (1u << s) + j);
+#pragma unroll
+            for (int k = j * 2 * half; k < j * 2 * half + half; k++) {
+                const bool in8 = b8[k] || b8[k + half];
+#pragma unroll
+                for (int c = 0; c < CPT; c++) gs_bfly_b(v[c][k], v[c][k + half], w, M, in8);
+                b8[k] = true;
+                b8[k + half] = false;
+            }
+        }
+    }
+}
 
 template <int KA, bool INV, int CPT, bool SPQ>
 __global__ __launch_bounds__(256) void k_cols(PlanArgs P, const u64* src, u64* dst, u32 batch, u32 nwg) {
@@ -883,11 +907,20 @@ __global__ __launch_bounds__(256) void k_cols(PlanArgs P, const u64* src, u64* d
     if (!INV) {
         cols_fwd<E, CPT>(v, P.tw + (u64)t * N * 2, M);
     } else {
-        cols_inv<E, CPT>(v, P.itw + (u64)t * N * 2, M);
+        if (OFHE_LAZY_GS) {
+            bool b8[E];
+            cols_inv_b<E, CPT>(v, b8, P.itw + (u64)t * N * 2, M);
 #pragma unroll
-        for (int k = 0; k < E; k++)
+            for (int k = 0; k < E; k++)
 #pragma unroll
-            for (int c = 0; c < CPT; c++) v[c][k] = canon4(v[c][k], q);
+                for (int c = 0; c < CPT; c++) v[c][k] = b8[k] ? canon8(v[c][k], q) : canon4(v[c][k], q);
+        } else {
+            cols_inv<E, CPT>(v, P.itw + (u64)t * N * 2, M);
+#pragma unroll
+            for (int k = 0; k < E; k++)
+#pragma unroll
+                for (int c = 0; c < CPT; c++) v[c][k] = canon4(v[c][k], q);
+        }
     }
 #pragma unroll
     for (int k = 0; k < E; k++) {
