@@ -290,7 +290,7 @@ __device__ __forceinline__ u64 twist_out(u64 x, Tw f, const Mod<SPQ>& M) {
 // (k, k + 2^(3-s)); its twiddle index is 2^s * M0 + (k >> (4 - s)) with
 // M0 = N/(16 st) + (global index of the 16*st super-group).
 // ---------------------------------------------------------------------------
-template <int S, class M_>
+template <int S, class M_, int CS = S & 1>
 __device__ __forceinline__ void fwd_stage16(u64 (&v)[16], const u64* tw, u32 M0, const M_& M) {
     constexpr int half = 8 >> S;
     const u64* base = tw + 2 * ((u64)M0 << S);  // one address per stage, j as immediate offsets
@@ -298,7 +298,7 @@ __device__ __forceinline__ void fwd_stage16(u64 (&v)[16], const u64* tw, u32 M0,
     for (int j = 0; j < (1 << S); j++) {
         Tw w = ldtw(base, j);
 #pragma unroll
-        for (int k = j * 2 * half; k < j * 2 * half + half; k++) ct_bfly<S & 1>(v[k], v[k + half], w, M);
+        for (int k = j * 2 * half; k < j * 2 * half + half; k++) ct_bfly<CS>(v[k], v[k + half], w, M);
     }
 }
 
@@ -357,6 +357,20 @@ template <class M_>
 __device__ __forceinline__ void fwd_round16(u64 (&v)[16], const u64* tw, u32 M0, const M_& M) {
     fwd_stage16<0>(v, tw, M0, M);
     fwd_stage16<1>(v, tw, M0, M);
+    fwd_stage16<2>(v, tw, M0, M);
+    fwd_stage16<3>(v, tw, M0, M);
+}
+// First round of a forward transform on canonical input (OFHE_FWD_CANON):
+// [0, q) -> 5q -> 9q -> 13q without a conditional subtract, then the CS stage
+// -> [0, 12q), the bound the alternating schedule leaves after any round.
+// Needs inputs < 4q (canonical, per the C ABI contract).
+#ifndef OFHE_FWD_CANON
+#define OFHE_FWD_CANON 1
+#endif
+template <class M_>
+__device__ __forceinline__ void fwd_round16_canon(u64 (&v)[16], const u64* tw, u32 M0, const M_& M) {
+    fwd_stage16<0>(v, tw, M0, M);
+    fwd_stage16<1, M_, OFHE_FWD_CANON ? 0 : 1>(v, tw, M0, M);
     fwd_stage16<2>(v, tw, M0, M);
     fwd_stage16<3>(v, tw, M0, M);
 }
@@ -674,7 +688,7 @@ __global__ __launch_bounds__(16 * TCOLS_W, OFHE_KB_WAVES) void k_tcols(PlanArgs 
         // round 1: rows h + 16k (p = tid + 16W k), stages m = 1..8
 #pragma unroll
         for (int k = 0; k < 16; k++) v[k] = ld_s(x + (u64)(h + 16 * k) * S + r);
-        fwd_round16(v, tw, 1, M);
+        fwd_round16_canon(v, tw, 1, M);
 #pragma unroll
         for (int k = 0; k < 16; k++) lds[L1 + 16 * W * k] = v[k];
         __syncthreads();
