@@ -96,3 +96,23 @@ def test_lazy_ct_alternating(q):
                     v[k], v[k + half] = a + t, a + 4 * q - t
                     assert v[k] < TWO64 and v[k + half] < TWO64
             assert max(v) < (12 if cs else 16) * q
+
+
+@pytest.mark.parametrize("q", [(1 << 60) - (1 << 17) + 1, (1 << 59) + 1])
+def test_fwd_first_round_canonical_input(q):
+    """fwd_round16_canon (OFHE_FWD_CANON): inputs < 4q, no conditional subtract
+    before the round's last stage, output < 12q like every other round"""
+    rng = random.Random(q ^ 2)
+    for _ in range(200):
+        v = [_worst(rng.randrange(q), q, 4 * q) for _ in range(16)]
+        for s in range(4):
+            cs = s == 3
+            half = 8 >> s
+            for base in range(0, 16, 2 * half):
+                for k in range(base, base + half):
+                    x, y = v[k], v[k + half]
+                    assert x < 16 * q and y < TWO64
+                    t = _worst(y * rng.randrange(1, q) % q, q, 4 * q)
+                    a = _csub(x, 8 * q) if cs else x
+                    v[k], v[k + half] = a + t, a + 4 * q - t
+        assert max(v) < 12 * q
