@@ -136,10 +136,39 @@ int ofhe_hip_modadd_vv(ofhe_plan_t plan, const uint64_t* a, const uint64_t* b, u
                        uint32_t batch, void* stream);
 int ofhe_hip_modsub_vv(ofhe_plan_t plan, const uint64_t* a, const uint64_t* b, uint64_t* c,
                        uint32_t batch, void* stream);
-/* c = a * s[t] mod q[t] with one scalar per tower (host array [towers]):
- * NativeVectorT::ModMul(const IntegerType&) (mubintvecnat.cpp:310-332, Shoup). */
+/* Vector (.) scalar with one scalar per tower (host array s[towers], any
+ * uint64_t; each is reduced mod q[t] first, as the reference does).  The
+ * scalars travel in the kernel arguments: nothing is staged, nothing
+ * synchronises, and c may alias a.  They replace the DPU SCALAR / SCALAR_EQ
+ * kernels (src/core/pim/dpu/element-wise/add-mod.c:23-100, sub-mod.c,
+ * mult-mod.c) and the CPU loops of
+ *   c = a * s mod q: NativeVectorT::ModMul(Eq)(const IntegerType&)
+ *                    (mubintvecnat.cpp:310-332, Shoup), DCRTPoly::Times(Integer);
+ *   c = a + s mod q: NativeVectorT::ModAdd(Eq)(const IntegerType&)
+ *                    (mubintvecnat.cpp:198-219), DCRTPoly::Plus(Integer) in
+ *                    evaluation form (dcrtpoly.h:162-163, poly-impl.h:213-220);
+ *   c = a - s mod q: NativeVectorT::ModSub(Eq)(const IntegerType&)
+ *                    (mubintvecnat.cpp:267-288), DCRTPoly::Minus(Integer)
+ *                    (dcrtpoly.h:182-183, poly-impl.h:223-227). */
 int ofhe_hip_modmul_scalar(ofhe_plan_t plan, const uint64_t* a, const uint64_t* s, uint64_t* c,
                            uint32_t batch, void* stream);
+int ofhe_hip_modadd_scalar(ofhe_plan_t plan, const uint64_t* a, const uint64_t* s, uint64_t* c,
+                           uint32_t batch, void* stream);
+int ofhe_hip_modsub_scalar(ofhe_plan_t plan, const uint64_t* a, const uint64_t* s, uint64_t* c,
+                           uint32_t batch, void* stream);
+/* c[index] = a[index] + s[t] mod q[t] in every (batch, tower); no other word is
+ * written (use in place, or copy a to c first): NativeVectorT::ModAddAtIndex(Eq)
+ * (mubintvecnat.cpp:221-231), i.e. PolyImpl / DCRTPoly::Plus(Integer) in
+ * coefficient form (poly-impl.h:213-220: a constant added to coefficient 0). */
+int ofhe_hip_modadd_scalar_at(ofhe_plan_t plan, const uint64_t* a, uint64_t index, const uint64_t* s,
+                              uint64_t* c, uint32_t batch, void* stream);
+
+/* Synthetic inputs for benchmarks and tests, no reference
+ * counterpart: dst[b][t][i] = splitmix64 draw i + 1 of the stream seeded
+ * 0x5EED ^ ((batch_offset + b) << 20) ^ (t << 8) ^ seed, mod q[t] -- what the
+ * CPU oracle's generator (oracle_fill_uniform) produces for the same seed. */
+int ofhe_hip_fill_uniform(ofhe_plan_t plan, uint64_t* dst, uint32_t batch, uint32_t batch_offset, uint64_t seed,
+                          void* stream);
 
 /* The metric pipeline, per (batch, tower): c = INTT(NTT(a) (.) b), a in
  * coefficient form, b in evaluation form, c in coefficient form.  Equals
@@ -183,7 +212,8 @@ int ofhe_hip_approx_mod_up(ofhe_plan_t plan_q, ofhe_plan_t plan_p, ofhe_bconv_t 
  * plan_p's basis to plan_q's (PHatInvModp, PHatModq); p_inv_modq: host
  * [Q] = P^-1 mod q_i.  t = 0 for CKKS / BFV; t > 0 (BGV) multiplies the P part
  * by t^-1 mod p_j and the switched part by t (t_inv_modp derived here).
- * Synchronises `stream` once to stage its small constant tables. */
+ * The small constant tables are built and uploaded on the first call with a
+ * given (t, p_inv_modq) and cached in p_to_q; no call synchronises. */
 int ofhe_hip_approx_mod_down(ofhe_plan_t plan_q, ofhe_plan_t plan_p, ofhe_bconv_t p_to_q,
                              const uint64_t* p_inv_modq, uint64_t t, const uint64_t* x, uint64_t* out,
                              uint32_t batch, void* stream);

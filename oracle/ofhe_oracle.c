@@ -315,6 +315,16 @@ void oracle_vec_modmul_scalar(const u64* a, u64 s, u64* c, u64 n, u64 q) {
     u64 sp = oracle_shoup_prep(s, q);
     for (u64 i = 0; i < n; i++) c[i] = oracle_modmul_shoup(a[i], s, q, sp);
 }
+/* scalar ModAdd(Eq) / ModSub(Eq), mubintvecnat.cpp:198-219, 267-288: the scalar is
+ * reduced (ModEq) when >= q, then ModAddFast / ModSubFastEq per element. */
+void oracle_vec_modadd_scalar(const u64* a, u64 s, u64* c, u64 n, u64 q) {
+    if (s >= q) s %= q;
+    for (u64 i = 0; i < n; i++) c[i] = oracle_modadd(a[i], s, q);
+}
+void oracle_vec_modsub_scalar(const u64* a, u64 s, u64* c, u64 n, u64 q) {
+    if (s >= q) s %= q;
+    for (u64 i = 0; i < n; i++) c[i] = oracle_modsub(a[i], s, q);
+}
 
 /* ---------------------------------------------------------------------------
  * DCRT (towers) level, [B][T][N] contiguous, OpenMP over (batch, tower) as the

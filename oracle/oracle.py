@@ -53,6 +53,8 @@ def lib() -> ctypes.CDLL:
             "oracle_vec_modadd": (None, [_u64p, _u64p, _u64p, _u64, _u64]),
             "oracle_vec_modsub": (None, [_u64p, _u64p, _u64p, _u64, _u64]),
             "oracle_vec_modmul_scalar": (None, [_u64p, _u64, _u64p, _u64, _u64]),
+            "oracle_vec_modadd_scalar": (None, [_u64p, _u64, _u64p, _u64, _u64]),
+            "oracle_vec_modsub_scalar": (None, [_u64p, _u64, _u64p, _u64, _u64]),
             "oracle_dcrt_ntt_fwd": (None, [_u64p, _u64, _u64, ctypes.c_uint, _u64p, _u64p, _u64p]),
             "oracle_dcrt_ntt_inv": (None, [_u64p, _u64, _u64, ctypes.c_uint, _u64p, _u64p, _u64p, _u64p, _u64p]),
             "oracle_dcrt_ntt_mul_intt": (None, [_u64p, _u64p, _u64p, _u64, _u64, ctypes.c_uint, _u64p, _u64p,
@@ -191,12 +193,40 @@ def eltwise(op: str, a: np.ndarray, b: np.ndarray, moduli) -> np.ndarray:
     return c
 
 
-def mul_scalar(a: np.ndarray, scalars, moduli) -> np.ndarray:
+def _scalar(fn: str, a: np.ndarray, scalars, moduli) -> np.ndarray:
     a = np.ascontiguousarray(a, dtype=np.uint64)
     c = np.empty_like(a)
+    f = getattr(lib(), fn)
     for bi in range(a.shape[0]):
         for t in range(a.shape[1]):
-            lib().oracle_vec_modmul_scalar(P(a[bi, t]), int(scalars[t]), P(c[bi, t]), a.shape[2], int(moduli[t]))
+            f(P(a[bi, t]), int(scalars[t]), P(c[bi, t]), a.shape[2], int(moduli[t]))
+    return c
+
+
+def mul_scalar(a: np.ndarray, scalars, moduli) -> np.ndarray:
+    """NativeVectorT::ModMul(const IntegerType&) per tower (mubintvecnat.cpp:310-332)."""
+    return _scalar("oracle_vec_modmul_scalar", a, scalars, moduli)
+
+
+def add_scalar(a: np.ndarray, scalars, moduli) -> np.ndarray:
+    """NativeVectorT::ModAdd(const IntegerType&) per tower (mubintvecnat.cpp:198-219)."""
+    return _scalar("oracle_vec_modadd_scalar", a, scalars, moduli)
+
+
+def sub_scalar(a: np.ndarray, scalars, moduli) -> np.ndarray:
+    """NativeVectorT::ModSub(const IntegerType&) per tower (mubintvecnat.cpp:267-288)."""
+    return _scalar("oracle_vec_modsub_scalar", a, scalars, moduli)
+
+
+def add_scalar_at(a: np.ndarray, index: int, scalars, moduli) -> np.ndarray:
+    """NativeVectorT::ModAddAtIndex(index, s_t) per tower (mubintvecnat.cpp:221-231): NativeIntegerT::ModAddEq
+    (ubintnat.h:726-737) on one word; Python big ints (small case)."""
+    c = np.array(a, dtype=np.uint64, copy=True)
+    for t in range(c.shape[1]):
+        q = int(moduli[t])
+        for bi in range(c.shape[0]):
+            x, s = int(c[bi, t, index]), int(scalars[t])
+            c[bi, t, index] = ((x % q) + (s % q)) % q
     return c
 
 

@@ -9,6 +9,8 @@ Two kinds of fixture live here:
      - UnitTestTransform.cpp:60-94  CRT_polynomial_mult KAT (q=113, m=8)
      - UnitTestMubintvec.cpp:276-359 1-limb vector ModAdd/ModSub/ModMul KAT
      - UnitTestNTT.cpp:53-133 round-trip inputs
+     - UnitTestPolyElements.cpp:265-305 SwitchModulus KAT, 500-523
+       AutomorphismTransform KAT (q=73, m=8)
      - SURVEY.md §8(c) probe outputs (moduli, minimal roots, y[0], y[1], c[0][0])
 2. Oracle outputs (oracle/ofhe_oracle.c) at small sizes, used as committed
    golden vectors for the GPU parity tests (regenerate with this script; the
@@ -56,6 +58,19 @@ def reference_fixtures():
             "x1": [431, 3414, 1234, 7845, 2145, 7415, 5471, 8452],
             "x2": [4127, 9647, 1987, 5410, 6541, 7014, 9741, 1256],
             "single_crt_bits": 22, "double_crt_bits": 28,
+        },
+        "kat_switch_modulus": {
+            "ref": "src/core/unittest/UnitTestPolyElements.cpp:265-305",
+            "q": 73, "m": 8, "root": 22,
+            "cases": [
+                {"x": [56, 1, 37, 2], "new_q": 17, "new_root": 15, "expected": [0, 1, 15, 2]},
+                {"x": [56, 43, 35, 28], "new_q": 193, "new_root": 150, "expected": [176, 163, 35, 28]},
+            ],
+        },
+        "kat_automorphism": {
+            "ref": "src/core/unittest/UnitTestPolyElements.cpp:500-523",
+            "q": 73, "m": 8, "root": 22, "format": "coefficient",
+            "x": [56, 1, 37, 2], "k": 3, "expected": [56, 2, 36, 1],
         },
         "survey_probes": {
             "ref": "SURVEY.md §8(c) (reference native code run in the survey container)",

@@ -161,3 +161,29 @@ def test_key_switch_param_errors():
     q, rq, p, rp = _bases(3, 5, 1)
     with pytest.raises(ValueError):
         K.KeySwitchParams(8, q, rq, p, rp, 4)  # ceil(5/4)=2: 5 - 2*3 <= 0
+
+
+def test_switch_modulus_reference_kat():
+    """UnitTestPolyElements.cpp:265-305: {56,1,37,2} mod 73 -> mod 17 = {0,1,15,2};
+    {56,43,35,28} mod 73 -> mod 193 = {176,163,35,28}."""
+    from conftest import load_golden
+
+    k = load_golden("reference_fixtures.json")["kat_switch_modulus"]
+    for c in k["cases"]:
+        got = K.switch_modulus(np.array(c["x"], np.uint64), k["q"], c["new_q"])
+        assert got.tolist() == c["expected"]
+
+
+def test_automorphism_reference_kat():
+    """UnitTestPolyElements.cpp:500-523: AutomorphismTransform(3) of {56,1,37,2}
+    mod 73 in coefficient form = {56,2,36,1}; and the evaluation-form map agrees
+    with it through the NTT (q = 73, m = 8, root 22)."""
+    from conftest import load_golden
+
+    k = load_golden("reference_fixtures.json")["kat_automorphism"]
+    x = np.array(k["x"], np.uint64)
+    assert K.automorphism(x, k["k"], False, k["q"]).tolist() == k["expected"]
+    tb = O.Tables(4, [k["q"]], [k["root"]])
+    ev = O.ntt_fwd(x.reshape(1, 1, 4), tb).reshape(-1)
+    back = O.ntt_inv(K.automorphism(ev, k["k"], True, k["q"]).reshape(1, 1, 4), tb).reshape(-1)
+    assert back.tolist() == k["expected"]

@@ -10,10 +10,13 @@
 
 namespace ofhe {
 
-enum { ELT_MUL = 0, ELT_ADD = 1, ELT_SUB = 2, ELT_MULS = 3 };
+enum { ELT_MUL = 0, ELT_ADD = 1, ELT_SUB = 2, ELT_MULS = 3, ELT_ADDS = 4, ELT_SUBS = 5 };
 
-// a, b, c: [batch][towers][N]; for ELT_MULS, b is a device array of
-// (s_t, s_t') pairs, one per tower.
+// ModAddFastEq (ubintnat.h:760-767) and ModSubFastEq (934-938) on canonical operands
+__device__ __forceinline__ u64 modadd_fast(u64 a, u64 b, u64 q) { return csub(a + b, q); }
+__device__ __forceinline__ u64 modsub_fast(u64 a, u64 b, u64 q) { return a < b ? a + q - b : a - b; }
+
+// a, b, c: [batch][towers][N], vector (.) vector.
 template <int OP>
 __global__ __launch_bounds__(256) void k_eltwise(const TowerConst* __restrict__ tcs,
                                                  const u64* a, const u64* b, u64* c, u64 npairs,
@@ -24,25 +27,94 @@ __global__ __launch_bounds__(256) void k_eltwise(const TowerConst* __restrict__ 
         const u32 t = (u32)((e >> log_n) % towers);
         const TowerConst tc = tcs[t];
         const ulonglong2 x = reinterpret_cast<const ulonglong2*>(a)[i];
+        const ulonglong2 y = reinterpret_cast<const ulonglong2*>(b)[i];
         ulonglong2 r;
-        if (OP == ELT_MULS) {
-            const u64 s = b[2 * t], sp = b[2 * t + 1];
-            r.x = shoup_canon(x.x, s, sp, tc.q);
-            r.y = shoup_canon(x.y, s, sp, tc.q);
+        if (OP == ELT_MUL) {
+            r.x = barrett_ref(x.x, y.x, tc.q, tc.mu, tc.nshift);
+            r.y = barrett_ref(x.y, y.y, tc.q, tc.mu, tc.nshift);
+        } else if (OP == ELT_ADD) {
+            r.x = modadd_fast(x.x, y.x, tc.q);
+            r.y = modadd_fast(x.y, y.y, tc.q);
         } else {
-            const ulonglong2 y = reinterpret_cast<const ulonglong2*>(b)[i];
-            if (OP == ELT_MUL) {
-                r.x = barrett_ref(x.x, y.x, tc.q, tc.mu, tc.nshift);
-                r.y = barrett_ref(x.y, y.y, tc.q, tc.mu, tc.nshift);
-            } else if (OP == ELT_ADD) {  // ModAddFastEq, ubintnat.h:760-767
-                r.x = csub(x.x + y.x, tc.q);
-                r.y = csub(x.y + y.y, tc.q);
-            } else {  // ModSubFastEq, ubintnat.h:934-938
-                r.x = x.x < y.x ? x.x + tc.q - y.x : x.x - y.x;
-                r.y = x.y < y.y ? x.y + tc.q - y.y : x.y - y.y;
-            }
+            r.x = modsub_fast(x.x, y.x, tc.q);
+            r.y = modsub_fast(x.y, y.y, tc.q);
         }
         reinterpret_cast<ulonglong2*>(c)[i] = r;
+    }
+}
+
+// Vector (.) scalar with one scalar per tower, the scalars passed by value in
+// the kernel arguments (no device table, so no upload to order against other
+// launches): ModMul(const IntegerType&) (Shoup, mubintvecnat.cpp:310-332),
+// ModAdd(Eq) / ModSub(Eq)(const IntegerType&) (mubintvecnat.cpp:198-219, 267-288), the
+// DPU SCALAR kernels of src/core/pim/dpu/element-wise/{add,sub,mult}-mod.c.
+// One launch covers towers [t0, t0 + cnt) of every batch entry (cnt <=
+// SCALAR_MAX); the host splits wider plans into several launches.
+constexpr u32 SCALAR_MAX = 96;  // 96 x 24 B = 2304 B of kernel arguments
+struct ScalarPack {
+    u64 v[3 * SCALAR_MAX];  // per tower of the range: q, s (reduced mod q), Shoup precon of s
+};
+template <int OP>
+__global__ __launch_bounds__(256) void k_scalar(ScalarPack S, const u64* a, u64* c, u64 npairs, u32 log_n,
+                                                u32 cnt, u32 t0, u32 towers) {
+    const u64 stride = (u64)gridDim.x * blockDim.x;
+    const u64 mask = (1ull << log_n) - 1;
+    for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < npairs; i += stride) {
+        const u64 e = 2 * i;
+        const u64 row = e >> log_n;  // b * cnt + tl
+        const u32 tl = (u32)(row % cnt);
+        const u64 b = row / cnt;
+        const u64 at = ((b * towers + t0 + tl) << log_n) | (e & mask);
+        const u64 q = S.v[3 * tl], s = S.v[3 * tl + 1];
+        const ulonglong2 x = *reinterpret_cast<const ulonglong2*>(a + at);
+        ulonglong2 r;
+        if (OP == ELT_MULS) {
+            const u64 sp = S.v[3 * tl + 2];
+            r.x = shoup_canon(x.x, s, sp, q);
+            r.y = shoup_canon(x.y, s, sp, q);
+        } else if (OP == ELT_ADDS) {
+            r.x = modadd_fast(x.x, s, q);
+            r.y = modadd_fast(x.y, s, q);
+        } else {
+            r.x = modsub_fast(x.x, s, q);
+            r.y = modsub_fast(x.y, s, q);
+        }
+        *reinterpret_cast<ulonglong2*>(c + at) = r;
+    }
+}
+
+// NativeVectorT::ModAddAtIndex(Eq)(i, b) (mubintvecnat.cpp:221-231): c[idx] of every
+// (batch, tower) = a[idx] + s_t mod q_t -- what PolyImpl::Plus(Integer) does in
+// coefficient form (poly-impl.h:213-220).  One thread per (batch, tower) of the
+// range; the other words are the caller's (in place, or copied beforehand).
+static __global__ __launch_bounds__(256) void k_scalar_at(ScalarPack S, const u64* a, u64* c, u32 batch, u32 log_n,
+                                                   u32 cnt, u32 t0, u32 towers, u64 idx) {
+    const u64 r = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= (u64)batch * cnt) return;
+    const u32 tl = (u32)(r % cnt);
+    const u64 b = r / cnt;
+    const u64 at = ((b * towers + t0 + tl) << log_n) + idx;
+    c[at] = modadd_fast(a[at], S.v[3 * tl + 1], S.v[3 * tl]);
+}
+
+// Synthetic uniform residues (bench / tests): word i of tower
+// t of batch entry b is splitmix64 draw i + 1 of the stream seeded
+// 0x5EED ^ (b << 20) ^ (t << 8) ^ seed, mod q_t -- the same numbers as the
+// oracle's sequential generator (splitmix64 is counter-based: draw k mixes
+// seed + k * 0x9E3779B97F4A7C15).
+static __global__ __launch_bounds__(256) void k_fill_uniform(const TowerConst* __restrict__ tcs, u64* dst, u64 words,
+                                                      u32 log_n, u32 towers, u32 b0, u64 seed) {
+    const u64 stride = (u64)gridDim.x * blockDim.x;
+    for (u64 e = (u64)blockIdx.x * blockDim.x + threadIdx.x; e < words; e += stride) {
+        const u64 row = e >> log_n;
+        const u32 t = (u32)(row % towers);
+        const u64 b = row / towers + b0;
+        const u64 i = e & ((1ull << log_n) - 1);
+        u64 z = (0x5EEDull ^ (b << 20) ^ ((u64)t << 8) ^ seed) + (i + 1) * 0x9E3779B97F4A7C15ull;
+        z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+        z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+        z ^= z >> 31;
+        dst[e] = z % tcs[t].q;
     }
 }
 

@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 
 #include <atomic>
+#include <map>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -102,8 +103,6 @@ struct ofhe_plan_s {
     ofhe::u64* d_twist_r = nullptr; // the same times 2^64 mod q (fused pipeline, Montgomery Hadamard)
     // host copies (for ofhe_hip_plan_tables and scalar prep)
     std::vector<ofhe::u64> q, psi, tab, tab_pre, itab, itab_pre, ninv;
-    ofhe::u64* d_scal = nullptr;  // scratch for per-tower scalars (modmul_scalar)
-    std::mutex scal_mu;
     // pipeline tuning (ofhe_hip_plan_tune): batch entries per chunk (0 = all)
     // and internal streams the chunks alternate over (1 = caller's stream).
     ofhe::u32 chunk_batch = 0, nstreams = 1;
@@ -117,8 +116,10 @@ struct ofhe_bconv_s {
     ofhe_ctx_t ctx = nullptr;
     ofhe::BconvArgs args{};
     ofhe::u64* d_mem = nullptr;
-    // per-call constant tables of ofhe_hip_approx_mod_down (grow-only)
+    // ofhe_hip_approx_mod_down's constant tables (P^-1 mod q_i, and for t > 0
+    // t^-1 mod p_j, t mod q_i), uploaded once per distinct (t, P^-1 mod q)
+    // into memory no launch has read yet and kept until destroy, so steady-state
+    // calls upload nothing and never synchronise
     std::mutex tab_mu;
-    ofhe::u64* d_tab = nullptr;
-    size_t tab_words = 0;
+    std::map<std::vector<ofhe::u64>, ofhe::u64*> tabs;
 };

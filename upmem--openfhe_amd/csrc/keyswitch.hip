@@ -163,34 +163,38 @@ int ofhe_hip_approx_mod_down(ofhe_plan_t pq, ofhe_plan_t pp, ofhe_bconv_t bc, co
     HIPCHK(hipSetDevice(pq->ctx->device));
     hipStream_t s = pick(stream);
     const u32 Q = pq->towers, P = pp->towers;
-    std::vector<TowerScalar> tab(Q + (t ? P + Q : 0));
-    for (u32 i = 0; i < Q; i++) tab[i] = scalar_of(pq->q[i], p_inv_modq[i]);
-    if (t) {
-        for (u32 j = 0; j < P; j++) tab[Q + j] = scalar_of(pp->q[j], invmod(t % pp->q[j], pp->q[j]));  // tInvModp
-        for (u32 i = 0; i < Q; i++) tab[Q + P + i] = scalar_of(pq->q[i], t);                          // t mod q_i
+    // Tables cached per (t, P^-1 mod q) in the converter: the first call with
+    // a key uploads into freshly allocated memory (no launch reads it yet, so
+    // the blocking copy cannot race); later calls only look the table up.
+    std::vector<u64> key(p_inv_modq, p_inv_modq + Q);
+    key.push_back(t);
+    u64* dtab = nullptr;
+    {
+        std::lock_guard<std::mutex> lk(bc->tab_mu);
+        auto it = bc->tabs.find(key);
+        if (it != bc->tabs.end()) {
+            dtab = it->second;
+        } else {
+            std::vector<TowerScalar> tab(Q + (t ? P + Q : 0));
+            for (u32 i = 0; i < Q; i++) tab[i] = scalar_of(pq->q[i], p_inv_modq[i]);
+            if (t) {
+                for (u32 j = 0; j < P; j++) tab[Q + j] = scalar_of(pp->q[j], invmod(t % pp->q[j], pp->q[j]));  // tInvModp
+                for (u32 i = 0; i < Q; i++) tab[Q + P + i] = scalar_of(pq->q[i], t);  // t mod q_i
+            }
+            const size_t words = tab.size() * 3;
+            HIPCHK(hipMalloc(&dtab, words * sizeof(u64)));
+            hipError_t e = hipMemcpy(dtab, tab.data(), words * sizeof(u64), hipMemcpyHostToDevice);
+            if (e != hipSuccess) {
+                (void)hipFree(dtab);
+                return fail(OFHE_ERR_HIP, std::string("mod-down tables: ") + hipGetErrorString(e));
+            }
+            bc->tabs.emplace(std::move(key), dtab);
+        }
     }
-    // Constant tables live in the converter (grow-only) and are written with
-    // a blocking copy after draining the device: a copy from pageable memory
-    // into stream-ordered (pool) memory was observed to race with the
-    // kernels that read it.  The lock keeps concurrent callers of this
-    // converter from overwriting each other's tables.
-    std::lock_guard<std::mutex> lk(bc->tab_mu);
-    const size_t words = tab.size() * 3;
-    if (bc->tab_words < words) {
-        HIPCHK(hipDeviceSynchronize());
-        (void)hipFree(bc->d_tab);
-        bc->d_tab = nullptr;
-        bc->tab_words = 0;
-        HIPCHK(hipMalloc(&bc->d_tab, words * sizeof(u64)));
-        bc->tab_words = words;
-    }
-    HIPCHK(hipDeviceSynchronize());
-    HIPCHK(hipMemcpy(bc->d_tab, tab.data(), words * sizeof(u64), hipMemcpyHostToDevice));
-    const TowerScalar* d = (const TowerScalar*)bc->d_tab;
+    const TowerScalar* d = (const TowerScalar*)dtab;
     ModDownArgs A{pq, pp, 0, 0, Q, P, bc->args, d, t ? d + Q : nullptr, t ? d + Q + P : nullptr};
     const u64 N = 1ull << pq->log_n;
     RCCHK(mod_down_run(A, x, (u64)(Q + P) * N, out, (u64)Q * N, batch, s));
-    HIPCHK(hipStreamSynchronize(s));  // the tables stay in use until the kernels finish
     return OFHE_OK;
 }
 

@@ -303,7 +303,6 @@ int ofhe_hip_plan_create(ofhe_ctx_t ctx, uint32_t log_n, uint32_t towers, const 
     if (e == hipSuccess) e = hipMemcpy(p->d_dtw, dtw.data(), sizeof(u64) * 2 * TN, hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMemcpy(p->d_twist, twist.data(), sizeof(u64) * 2 * TN, hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMemcpy(p->d_twist_r, twist_r.data(), sizeof(u64) * 2 * TN, hipMemcpyHostToDevice);
-    if (e == hipSuccess) e = hipMalloc(&p->d_scal, sizeof(u64) * 2 * towers);
     if (e == hipSuccess) e = hipMemcpy(p->d_tc, tc.data(), sizeof(TowerConst) * towers, hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMemcpy(p->d_tw, tw.data(), sizeof(u64) * 2 * TN, hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMemcpy(p->d_itw, itw.data(), sizeof(u64) * 2 * TN, hipMemcpyHostToDevice);
@@ -347,7 +346,6 @@ int ofhe_hip_plan_destroy(ofhe_plan_t p) {
     (void)hipFree(p->d_dtw);
     (void)hipFree(p->d_twist);
     (void)hipFree(p->d_twist_r);
-    (void)hipFree(p->d_scal);
     delete p;
     return OFHE_OK;
 }
@@ -679,28 +677,74 @@ int ofhe_hip_modsub_vv(ofhe_plan_t p, const uint64_t* a, const uint64_t* b, uint
     return eltwise<ELT_SUB>(p, a, b, c, batch, stream);
 }
 
-int ofhe_hip_modmul_scalar(ofhe_plan_t p, const uint64_t* a, const uint64_t* s, uint64_t* c,
-                           uint32_t batch, void* stream) {
+// Vector (.) per-tower scalar.  Each scalar is reduced mod q_t first, as the
+// reference does (mubintvecnat.cpp:198-219, 267-288, 310-332), and travels in
+// the kernel arguments, SCALAR_MAX towers per launch: nothing is uploaded, so
+// concurrent calls on any streams never share state and nothing synchronises.
+template <int OP>
+static int scalar_op(ofhe_plan_t p, const u64* a, const u64* s, u64* c, u32 batch, bool at_index, u64 idx,
+                     void* stream) {
     int rc = check_common(p, batch);
     if (rc) return rc;
+    if (!a || !c) return fail(OFHE_ERR_ARG, "NULL data pointer");
     if (!s) return fail(OFHE_ERR_ARG, "scalar array is NULL");
-    // ModMul(const IntegerType&) reduces the scalar first, then Shoup
-    // (mubintvecnat.cpp:310-332).
-    std::vector<u64> sp(2 * p->towers);
-    for (u32 t = 0; t < p->towers; t++) {
-        const u64 v = s[t] % p->q[t];
-        sp[2 * t] = v;
-        sp[2 * t + 1] = shoup_pre(v, p->q[t]);
-    }
-    // the scalar table is tiny; it rides on the same stream, serialised by
-    // the plan's mutex so concurrent callers on one plan do not race on it.
-    std::lock_guard<std::mutex> lk(p->scal_mu);
+    if (at_index && idx >= (1ull << p->log_n)) return fail(OFHE_ERR_ARG, "index out of range");
     HIPCHK(hipSetDevice(p->ctx->device));
-    // an earlier modmul_scalar (on any stream) may still read d_scal: drain
-    // the device, then a blocking copy
-    HIPCHK(hipDeviceSynchronize());
-    HIPCHK(hipMemcpy(p->d_scal, sp.data(), sizeof(u64) * sp.size(), hipMemcpyHostToDevice));
-    return eltwise<ELT_MULS>(p, a, p->d_scal, c, batch, stream);
+    hipStream_t st = pick(stream);
+    for (u32 t0 = 0; t0 < p->towers; t0 += SCALAR_MAX) {
+        const u32 cnt = p->towers - t0 < SCALAR_MAX ? p->towers - t0 : SCALAR_MAX;
+        ScalarPack S{};
+        for (u32 i = 0; i < cnt; i++) {
+            const u64 q = p->q[t0 + i], v = s[t0 + i] % q;
+            S.v[3 * i] = q;
+            S.v[3 * i + 1] = v;
+            S.v[3 * i + 2] = shoup_pre(v, q);
+        }
+        if (at_index) {
+            const u64 rows = (u64)batch * cnt;
+            hipLaunchKernelGGL(k_scalar_at, dim3((u32)((rows + 255) / 256)), dim3(256), 0, st, S, a, c, batch,
+                               p->log_n, cnt, t0, p->towers, idx);
+        } else {
+            const u64 npairs = ((u64)batch * cnt << p->log_n) / 2;
+            u64 blocks = (npairs + 255) / 256;
+            if (blocks > 256 * 16) blocks = 256 * 16;
+            hipLaunchKernelGGL((k_scalar<OP>), dim3((u32)blocks), dim3(256), 0, st, S, a, c, npairs, p->log_n, cnt,
+                               t0, p->towers);
+        }
+        RCCHK(post_launch());
+    }
+    return OFHE_OK;
+}
+
+int ofhe_hip_modmul_scalar(ofhe_plan_t p, const uint64_t* a, const uint64_t* s, uint64_t* c,
+                           uint32_t batch, void* stream) {
+    return scalar_op<ELT_MULS>(p, a, s, c, batch, false, 0, stream);
+}
+int ofhe_hip_modadd_scalar(ofhe_plan_t p, const uint64_t* a, const uint64_t* s, uint64_t* c,
+                           uint32_t batch, void* stream) {
+    return scalar_op<ELT_ADDS>(p, a, s, c, batch, false, 0, stream);
+}
+int ofhe_hip_modsub_scalar(ofhe_plan_t p, const uint64_t* a, const uint64_t* s, uint64_t* c,
+                           uint32_t batch, void* stream) {
+    return scalar_op<ELT_SUBS>(p, a, s, c, batch, false, 0, stream);
+}
+int ofhe_hip_modadd_scalar_at(ofhe_plan_t p, const uint64_t* a, uint64_t index, const uint64_t* s, uint64_t* c,
+                              uint32_t batch, void* stream) {
+    return scalar_op<ELT_ADDS>(p, a, s, c, batch, true, index, stream);
+}
+
+int ofhe_hip_fill_uniform(ofhe_plan_t p, uint64_t* dst, uint32_t batch, uint32_t batch_offset, uint64_t seed,
+                          void* stream) {
+    int rc = check_common(p, batch);
+    if (rc) return rc;
+    if (!dst) return fail(OFHE_ERR_ARG, "NULL data pointer");
+    HIPCHK(hipSetDevice(p->ctx->device));
+    const u64 words = (u64)batch * p->towers << p->log_n;
+    u64 blocks = (words + 255) / 256;
+    if (blocks > 256 * 64) blocks = 256 * 64;
+    hipLaunchKernelGGL(k_fill_uniform, dim3((u32)blocks), dim3(256), 0, pick(stream), p->d_tc, dst, words,
+                       p->log_n, p->towers, batch_offset, seed);
+    return post_launch();
 }
 
 // ---------------------------------------------------------------------------
@@ -786,7 +830,7 @@ int ofhe_hip_bconv_destroy(ofhe_bconv_t b) {
     if (!b) return fail(OFHE_ERR_ARG, "bconv is NULL");
     if (b->ctx) (void)hipSetDevice(b->ctx->device);
     (void)hipFree(b->d_mem);
-    (void)hipFree(b->d_tab);
+    for (auto& kv : b->tabs) (void)hipFree(kv.second);
     delete b;
     return OFHE_OK;
 }

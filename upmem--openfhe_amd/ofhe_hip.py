@@ -71,6 +71,10 @@ _SIGS = {
     "ofhe_hip_modadd_vv": (ctypes.c_int, [_vp, _vp, _vp, _vp, ctypes.c_uint32, _vp]),
     "ofhe_hip_modsub_vv": (ctypes.c_int, [_vp, _vp, _vp, _vp, ctypes.c_uint32, _vp]),
     "ofhe_hip_modmul_scalar": (ctypes.c_int, [_vp, _vp, _u64p, _vp, ctypes.c_uint32, _vp]),
+    "ofhe_hip_modadd_scalar": (ctypes.c_int, [_vp, _vp, _u64p, _vp, ctypes.c_uint32, _vp]),
+    "ofhe_hip_modsub_scalar": (ctypes.c_int, [_vp, _vp, _u64p, _vp, ctypes.c_uint32, _vp]),
+    "ofhe_hip_modadd_scalar_at": (ctypes.c_int, [_vp, _vp, ctypes.c_uint64, _u64p, _vp, ctypes.c_uint32, _vp]),
+    "ofhe_hip_fill_uniform": (ctypes.c_int, [_vp, _vp, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint64, _vp]),
     "ofhe_hip_ntt_mul_intt": (ctypes.c_int, [_vp, _vp, _vp, _vp, ctypes.c_uint32, _vp]),
     "ofhe_hip_ntt_mul_intt_stage": (ctypes.c_int, [_vp, ctypes.c_int, _vp, _vp, _vp, ctypes.c_uint32, _vp]),
     "ofhe_hip_bconv_create": (ctypes.c_int, [_vp, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
@@ -285,6 +289,34 @@ class NTTPlan:
             raise MathError("one scalar per tower required")
         _check(lib().ofhe_hip_modmul_scalar(self.handle, _vp(a), _arr(scalars), _vp(c), int(batch),
                                             _vp(stream or None)))
+
+    def mod_add_scalar(self, a: int, scalars: Sequence[int], c: int, batch: int = 1, stream: int = 0) -> None:
+        """NativeVectorT::ModAdd(const IntegerType&) per tower (mubintvecnat.cpp:198-219)."""
+        if len(scalars) != self.towers:
+            raise MathError("one scalar per tower required")
+        _check(lib().ofhe_hip_modadd_scalar(self.handle, _vp(a), _arr(scalars), _vp(c), int(batch),
+                                            _vp(stream or None)))
+
+    def mod_sub_scalar(self, a: int, scalars: Sequence[int], c: int, batch: int = 1, stream: int = 0) -> None:
+        """NativeVectorT::ModSub(const IntegerType&) per tower (mubintvecnat.cpp:267-288)."""
+        if len(scalars) != self.towers:
+            raise MathError("one scalar per tower required")
+        _check(lib().ofhe_hip_modsub_scalar(self.handle, _vp(a), _arr(scalars), _vp(c), int(batch),
+                                            _vp(stream or None)))
+
+    def mod_add_scalar_at(self, a: int, index: int, scalars: Sequence[int], c: int, batch: int = 1,
+                          stream: int = 0) -> None:
+        """NativeVectorT::ModAddAtIndex(index, s_t) per tower (mubintvecnat.cpp:221-231); only word
+        `index` of each (batch, tower) of c is written."""
+        if len(scalars) != self.towers:
+            raise MathError("one scalar per tower required")
+        _check(lib().ofhe_hip_modadd_scalar_at(self.handle, _vp(a), int(index), _arr(scalars), _vp(c), int(batch),
+                                               _vp(stream or None)))
+
+    def fill_uniform(self, dst: int, batch: int, seed: int, batch_offset: int = 0, stream: int = 0) -> None:
+        """Synthetic residues: splitmix64 streams seeded 0x5EED ^ (b<<20) ^ (t<<8) ^ seed, mod q_t."""
+        _check(lib().ofhe_hip_fill_uniform(self.handle, _vp(dst), int(batch), int(batch_offset), int(seed),
+                                           _vp(stream or None)))
 
     # --- tower-range transforms on strided data ---
     def forward_range(self, t0: int, count: int, src: int, dst: int, src_stride: int, dst_stride: int,
