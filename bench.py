@@ -1,21 +1,28 @@
 #!/usr/bin/env python3
 """Headline benchmark: 64-bit coefficients/s for c = INTT(NTT(a) (.) b) on
 N = 2^16, 16 towers, batch 1024 per GPU (BASELINE.json configs[2]), with the
-dominant kernel's HBM-roofline fraction and a CPU baseline on the host cores.
+pipeline's HBM- and VALU-roofline fractions and a CPU baseline on the host cores.
 
-Single GPU:   python bench.py [--steps K --warmup W]
-N GPUs:       python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 \
-                  --master-port P bench.py --gpus N
-Each rank processes its own batch shard (weak scaling: per-GPU work fixed, no
-collective on the data path).  RCCL is used once at setup to broadcast a
-synthetic evaluation key from rank 0 (the only exchange the north star names).
+  python bench.py [--gpus N] [--steps K] [--warmup W]
 
-Prints ONE JSON line on rank 0.
+--gpus N > 1 without WORLD_SIZE in the environment starts N ranks itself
+(torch.distributed.run, one process per GPU) before anything touches the GPU;
+under an external launcher WORLD_SIZE must equal N.  Each rank runs its own
+batch (weak scaling, no data-path collective); the only collective is the
+RCCL evaluation-key broadcast at setup.  Secondary lines in
+the same JSON object: configs[3] (32 towers split over the ranks, strong
+scaling), configs[4] (HYBRID key switching, one bounded sample), configs[0]
+(CPU-only add / Hadamard, poly-benchmark semantics).
+
+Rank 0 prints ONE JSON line.
 """
 import argparse
+import hashlib
+import glob
 import json
 import os
 import socket
+import subprocess
 import sys
 import time
 
@@ -23,9 +30,26 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "upmem--openfhe_amd"))
 
 METRIC = "64-bit coeffs/sec for NTT+Hadamard+INTT, N=2^16, 16 towers; % HBM roofline"
-HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8 TB/s spec
+HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8 TB/s
 ALG_BYTES_PER_COEFF = 24       # read a, read b, write c
-STAGE_NAMES = {0: "colpass<fwd>", 1: "k_block<fused>", 2: "colpass<inv>"}  # colpass = k_tcols (N=2^16) or k_cols
+# per-launch algorithmic bytes per coefficient of the three pipeline kernels
+KERNEL_BYTES = {"colpass<fwd>": 16, "k_block<fused>": 24, "colpass<inv>": 16}
+STAGE_NAMES = {0: "colpass<fwd>", 1: "k_block<fused>", 2: "colpass<inv>"}  # colpass = k_tcols (2^16) or k_cols
+SIMDS = 1024                   # 256 CUs x 4 SIMDs
+VALU_ISSUE_CEILING = 0.25      # wave64 VALU instructions per SIMD per cycle (4-cycle issue)
+REF_CPU_MS_1T = 41.1           # reference NTT+Hadamard+INTT, 2^16 x 16 towers, 1 thread
+PMC_FILE = os.path.join(ROOT, "profiles", "pmc_current.json")
+
+
+def build_id() -> str:
+    """Hash of the backend's sources: PMC summaries are used only for the build they measured."""
+    h = hashlib.sha256()
+    csrc = os.path.join(ROOT, "upmem--openfhe_amd", "csrc")
+    for f in sorted(glob.glob(os.path.join(csrc, "*.hip")) + glob.glob(os.path.join(csrc, "*.hpp")) +
+                    [os.path.join(csrc, "Makefile"), os.path.join(ROOT, "include", "ofhe_hip.h")]):
+        h.update(os.path.basename(f).encode())
+        h.update(open(f, "rb").read())
+    return h.hexdigest()[:16]
 
 
 def moduli_chain(log_n, towers, bits=60):
@@ -82,7 +106,7 @@ def moduli_chain(log_n, towers, bits=60):
     return qs, roots
 
 
-def main():
+def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
@@ -92,19 +116,84 @@ def main():
     ap.add_argument("--batch", type=int, default=1024, help="polynomials per GPU")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget (0 = skip)")
     ap.add_argument("--no-check", action="store_true")
+    ap.add_argument("--no-extras", action="store_true",
+                    help="headline only: skip configs[3]/[4]/[0], PCIe and CPU legs (profiling passes)")
     ap.add_argument("--workload", default="pipeline", choices=["pipeline", "keyswitch"],
                     help="pipeline = the headline metric (configs[2]); keyswitch = configs[4] HYBRID "
-                         "key switching (secondary line, not the headline)")
+                         "key switching as the main line")
     ap.add_argument("--shard", default="batch", choices=["batch", "towers"],
                     help="batch = every rank runs its own batch of --batch (weak scaling, the default line); "
-                         "towers = configs[3]: --towers split across ranks, same batch on each (strong scaling)")
+                         "towers = configs[3] as the main line: --towers split across ranks (strong scaling)")
+    ap.add_argument("--c3-towers", type=int, default=32, help="configs[3] towers (split over ranks)")
+    ap.add_argument("--c3-batch", type=int, default=512, help="configs[3] polynomials (the same on every rank)")
     ap.add_argument("--ks-batch", type=int, default=8, help="ciphertext polynomials per GPU (keyswitch)")
+    ap.add_argument("--ks-steps", type=int, default=10, help="keyswitch sample steps in the default run")
     ap.add_argument("--pcie-batch", type=int, default=32, help="polynomials per chunk of the PCIe-inclusive run")
     ap.add_argument("--pcie-chunks", type=int, default=16, help="chunks of the PCIe-inclusive run (0 = skip)")
-    args = ap.parse_args()
-    if args.workload == "keyswitch":
-        return bench_keyswitch(args)
+    ap.add_argument("--launch-check", action="store_true",
+                    help="start the ranks and report them (gloo, no GPU): checks the --gpus launcher")
+    return ap.parse_args(argv)
 
+
+# ---------------------------------------------------------------------------
+# Launch: --gpus N starts N ranks itself unless an external launcher did
+# ---------------------------------------------------------------------------
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(n: int) -> int:
+    """One process per GPU through torch.distributed.run, started as a child
+    (this process has not touched the GPU); returns the launcher's exit code."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__)]
+    cmd += sys.argv[1:]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"))
+    return subprocess.call(cmd, env=env)
+
+
+def launch_check():
+    """Each rank joins a gloo group; rank 0 prints the ranks that came up."""
+    import torch.distributed as dist
+
+    dist.init_process_group("gloo")
+    world, rank = dist.get_world_size(), dist.get_rank()
+    info = [None] * world
+    dist.all_gather_object(info, {"rank": rank, "pid": os.getpid(), "local_rank": int(os.environ["LOCAL_RANK"])})
+    if rank == 0:
+        print(json.dumps({"launch_check": True, "n_gpus": world, "ranks": [i["rank"] for i in info],
+                          "local_ranks": [i["local_rank"] for i in info], "pids": [i["pid"] for i in info]}),
+              flush=True)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def main():
+    args = parse_args()
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus))
+    if env_world is not None and int(env_world) != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={env_world}; they must agree", file=sys.stderr)
+        sys.exit(2)
+    if args.launch_check:
+        if env_world is None:
+            print(json.dumps({"launch_check": True, "n_gpus": 1, "ranks": [0], "pids": [os.getpid()]}))
+            return
+        return launch_check()
+    if args.workload == "keyswitch":
+        return bench_keyswitch_main(args)
+    return bench_pipeline(args)
+
+
+# ---------------------------------------------------------------------------
+# Headline: configs[2]
+# ---------------------------------------------------------------------------
+def _dist_setup():
     import torch
     import torch.distributed as dist
 
@@ -116,18 +205,71 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
+    return world, rank, local, dev
+
+
+def _timed(step, steps, warmup, stream, world, dev):
+    """W untimed steps, then K steps bracketed by barrier + synchronize; returns
+    (max-over-ranks host seconds, launch-stream event ms per step)."""
+    import torch
+    import torch.distributed as dist
+
+    import shard
+
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    e0.record(stream)
+    for _ in range(steps):
+        step()
+    e1.record(stream)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        elapsed = shard.max_over_ranks(elapsed, device=dev)
+    return elapsed, e0.elapsed_time(e1) / steps
+
+
+def load_pmc(log_n, towers, batch):
+    """profiles/pmc_current.json (tools/pmc_round.sh) when it measured this build
+    and this configuration; else None with the reason."""
+    if not os.path.exists(PMC_FILE):
+        return None, "no profiles/pmc_current.json"
+    try:
+        pm = json.load(open(PMC_FILE))
+    except Exception as e:  # noqa: BLE001
+        return None, f"unreadable pmc file: {e}"
+    if pm.get("build_id") != build_id():
+        return None, f"pmc file measured build {pm.get('build_id')}, this is {build_id()}"
+    c = pm.get("config", {})
+    if (c.get("log_n"), c.get("towers"), c.get("batch")) != (log_n, towers, batch):
+        return None, f"pmc file measured {c}, this run is log_n={log_n} towers={towers} batch={batch}"
+    return pm, None
+
+
+def bench_pipeline(args):
+    import torch
+    import torch.distributed as dist
+
+    world, rank, local, dev = _dist_setup()
 
     import ofhe_hip as H
     import shard
 
     log_n, T_total, B = args.log_n, args.towers, args.batch
     if args.shard == "batch":
-        # weak scaling: every rank owns a batch shard of the same size
-        _, B_rank = shard.shard_batch(args.batch * world, rank, world)
+        b0, B_rank = shard.shard_batch(args.batch * world, rank, world)
         assert B_rank == args.batch
         t_start, T = 0, T_total
     else:
-        # strong scaling (configs[3]): a contiguous tower range per rank
+        b0 = 0
         t_start, T = shard.shard_towers(T_total, rank, world)
         if T == 0:
             raise SystemExit(f"--shard towers needs at least one tower per rank ({T_total} over {world})")
@@ -137,26 +279,24 @@ def main():
     qs_all, roots_all = moduli_chain(log_n, T_total)
     qs, roots = qs_all[t_start:t_start + T], roots_all[t_start:t_start + T]
     plan = H.NTTPlan(ctx, log_n, qs, roots)
-
-    # synthetic inputs, uniform residues mod q_t, generated on the device
-    g = torch.Generator(device=dev)
-    g.manual_seed(0x5EED + rank)
-    a = torch.empty((B, T, n), dtype=torch.int64, device=dev)
-    b = torch.empty((B, T, n), dtype=torch.int64, device=dev)
-    for t, q in enumerate(qs):
-        a[:, t, :].random_(0, q, generator=g)
-        b[:, t, :].random_(0, q, generator=g)
-    c = torch.empty_like(a)
     stream = torch.cuda.current_stream(dev)
     sp = stream.cuda_stream
 
-    # RCCL broadcast of a synthetic hybrid key-switching key (configs[3]; setup,
-    # outside the timed loop -- the only collective the path has)
+    # synthetic inputs, SURVEY.md §8(d): splitmix64 seed 0x5EED ^ (b<<20) ^ (t<<8) ^ operand,
+    # mod q_t, generated on the device (global batch index b)
+    a = torch.empty((B, T, n), dtype=torch.int64, device=dev)
+    b = torch.empty((B, T, n), dtype=torch.int64, device=dev)
+    plan.fill_uniform(a.data_ptr(), B, 1, b0, sp)
+    plan.fill_uniform(b.data_ptr(), B, 2, b0, sp)
+    c = torch.empty_like(a)
+
+    # RCCL broadcast of a synthetic hybrid key-switching key (setup, outside the
+    # timed loop -- the only collective the path has)
     bcast, comm = None, None
     if world > 1:
         key = torch.empty(shard.evalkey_words(T_total, log_n, 3), dtype=torch.int64, device=dev)
         if rank == 0:
-            key.random_(0, qs[-1], generator=g)
+            key.random_(0, qs[-1])
         bfn, backend, comm = shard.key_broadcaster(ctx, rank, world)
         dist.barrier()
         torch.cuda.synchronize()
@@ -170,27 +310,14 @@ def main():
     def step():
         plan.ntt_mul_intt(a.data_ptr(), b.data_ptr(), c.data_ptr(), B, sp)
 
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        elapsed = shard.max_over_ranks(elapsed, device=dev)
-    coeffs_per_step = B * T * n * world if args.shard == "batch" else B * T_total * n
+    elapsed, pipe_ms = _timed(step, args.steps, args.warmup, stream, world, dev)
+    coeffs_rank = B * T * n
+    coeffs_per_step = coeffs_rank * world if args.shard == "batch" else B * T_total * n
     value = coeffs_per_step * args.steps / elapsed
     ms_per_step = elapsed / args.steps * 1e3
 
     # per-kernel durations with HIP events on the launch stream (separate pass)
-    kernels = {}
+    kernels_ms = {}
     reps = max(3, min(args.steps, 10))
     for st in (0, 1, 2):
         if log_n <= 12 and st != 1:
@@ -203,34 +330,11 @@ def main():
             plan.ntt_mul_intt_stage(st, a.data_ptr(), b.data_ptr(), c.data_ptr(), B, sp)
         ev1.record(stream)
         ev1.synchronize()
-        kernels[STAGE_NAMES[st]] = ev0.elapsed_time(ev1) / reps
-    dominant = max(kernels, key=kernels.get)
-    kms = kernels[dominant]
-    coeffs_rank = B * T * n
-    achieved = ALG_BYTES_PER_COEFF * coeffs_rank / (kms * 1e-3) / 1e9
-    traffic = None
-    pmc_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    if os.path.exists(pmc_path):
-        try:
-            pm = json.load(open(pmc_path))
-            ent = pm.get("kernels", {}).get(dominant)
-            if ent and ent.get("batch") == B and ent.get("log_n") == log_n and ent.get("towers") == T:
-                traffic = ent.get("hbm_bytes_per_launch")
-        except Exception:
-            traffic = None
+        kernels_ms[STAGE_NAMES[st]] = ev0.elapsed_time(ev1) / reps
 
-    # VALU issue rate of the dominant kernel from the SQ counters
-    # (tools/pmc_valu.sh -> profiles/pmc_valu.json): the path is bound by
-    # integer-VALU issue, not HBM
-    valu = None
-    vpath = os.path.join(ROOT, "profiles", "pmc_valu.json")
-    if os.path.exists(vpath):
-        try:
-            valu = json.load(open(vpath)).get("kernels", {}).get(dominant)
-        except Exception:
-            valu = None
+    roofline = make_roofline(pipe_ms, kernels_ms, coeffs_rank, log_n, T, B)
 
-    # spot parity check against the oracle (one tower of two batch entries)
+    # spot parity check against the oracle (two (batch, tower) rows)
     parity = None
     if not args.no_check and rank == 0:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
@@ -245,39 +349,22 @@ def main():
             aa = a[bi, ti].cpu().numpy().view(np.uint64).reshape(1, 1, n)
             bb = b[bi, ti].cpu().numpy().view(np.uint64).reshape(1, 1, n)
             cc = c[bi, ti].cpu().numpy().view(np.uint64).reshape(1, 1, n)
+            want_a = O.splitmix_fill(n, qs[ti], O.U([0x5EED ^ ((b0 + bi) << 20) ^ ((t_start + ti) << 8) ^ 1]))
+            ok = ok and bool(np.array_equal(aa.reshape(-1), want_a))
             ok = ok and bool(np.array_equal(cc, O.ntt_mul_intt(aa, bb, tb)))
         parity = ok
 
-    # PCIe-inclusive rate (DESIGN.md §(d)): a and b in pinned host memory, c back
-    # to host, chunks pipelined over three streams (H2D, compute, D2H).  A side
-    # figure, never `value`.
-    pcie = None
-    if rank == 0 and world == 1 and args.pcie_chunks > 0 and B >= 2 * args.pcie_batch:
-        pcie = pcie_inclusive(plan, a, b, c, args.pcie_batch, args.pcie_chunks, dev)
-
-    # CPU baseline: the oracle (C, OpenMP over batch x towers) on a bounded sample
-    cpu = None
-    if rank == 0 and world == 1 and args.cpu_seconds > 0:
-        sys.path.insert(0, os.path.join(ROOT, "oracle"))
-        import numpy as np
-        import oracle as O
-
-        Bs = 4
-        tbs = O.Tables(n, qs, roots)
-        ca = O.uniform_dcrt(Bs, T, n, qs, 1)
-        cb = O.uniform_dcrt(Bs, T, n, qs, 2)
-        O.ntt_mul_intt(ca, cb, tbs)  # warm
-        runs, t0 = 0, time.perf_counter()
-        while True:
-            O.ntt_mul_intt(ca, cb, tbs)
-            runs += 1
-            el = time.perf_counter() - t0
-            if el >= args.cpu_seconds:
-                break
-        cpu = {"value": runs * Bs * T * n / el, "unit": "coeffs/s", "cores": int(O.lib().oracle_num_threads()),
-               "kind": "port",
-               "sample": f"{runs} runs x {Bs} polys x {T} towers x N=2^{log_n} ({el:.1f} s), "
-                         f"oracle/ofhe_oracle.c OpenMP over batch x towers, host {socket.gethostname()}"}
+    del a, b, c
+    torch.cuda.empty_cache()
+    extras = {}
+    if not args.no_extras:
+        extras["configs3"] = bench_configs3(args, ctx, world, rank, dev)
+        extras["keyswitch"] = bench_keyswitch(args, ctx, world, rank, dev, steps=args.ks_steps, warmup=2)
+        if rank == 0 and world == 1:
+            extras["pcie_inclusive"] = (pcie_inclusive(plan, args.pcie_batch, args.pcie_chunks, dev)
+                                        if args.pcie_chunks > 0 else None)
+            extras["configs0"] = bench_configs0(ctx)
+            extras["cpu_baseline"] = cpu_baseline(args, qs, roots, log_n, T) if args.cpu_seconds > 0 else None
 
     if rank == 0:
         out = {
@@ -292,7 +379,8 @@ def main():
             "scaling": "weak" if args.shard == "batch" else "strong",
             "vs_baseline": None,
             "dtype": "u64",
-            "data": "synthetic: uniform residues mod q_t (torch random_ on device), a coeff form, b eval form",
+            "data": "synthetic: splitmix64 residues mod q_t, seed 0x5EED^(b<<20)^(t<<8)^operand "
+                    "(SURVEY.md §8(d)), generated on the device; a coefficient form, b evaluation form",
             "config": ({"workload": f"configs[2]: N=2^{log_n}, towers={T}, batch={B} per GPU, "
                                     "c = INTT(NTT(a) (.) b)",
                         "log_n": log_n, "towers": T, "batch_per_gpu": B, "global_batch": B * world,
@@ -302,16 +390,16 @@ def main():
                                     f"batch={B}, c = INTT(NTT(a) (.) b)",
                         "log_n": log_n, "towers": T_total, "towers_rank0": T, "global_batch": B,
                         "parallelism": f"tower-sharded x{world} (no data-path collective)"}),
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": dominant,
-                         "kernel_ms": kms, "alg_bytes_per_launch": ALG_BYTES_PER_COEFF * coeffs_rank,
-                         "valu_issue": valu},
-            "pipeline_hbm_frac": value / world * ALG_BYTES_PER_COEFF / (HBM_PEAK_GBS * 1e9),
-            "kernels_ms": kernels,
-            "cpu_baseline": cpu,
-            "pcie_inclusive": pcie,
+            "roofline": roofline,
+            "kernels_ms": kernels_ms,
+            "cpu_baseline": extras.get("cpu_baseline"),
             "parity_spot_check": parity,
             "evalkey_broadcast": bcast,
+            "configs3": extras.get("configs3"),
+            "keyswitch": extras.get("keyswitch"),
+            "configs0": extras.get("configs0"),
+            "pcie_inclusive": extras.get("pcie_inclusive"),
+            "build_id": build_id(),
         }
         print(json.dumps(out), flush=True)
     if world > 1:
@@ -322,15 +410,358 @@ def main():
         dist.destroy_process_group()
 
 
-def pcie_inclusive(plan, a, b, c, bc, chunks, dev):
-    """c = INTT(NTT(a) (.) b) with a, b in pinned host memory and c returned to
-    it: chunk i's H2D, chunk i-1's pipeline and chunk i-2's D2H overlap on three
-    streams; device slots alternate over the first 2*bc entries of a, b, c.
-    Returns coefficients/s over `chunks` chunks of `bc` polynomials."""
+def make_roofline(pipe_ms, kernels_ms, coeffs_rank, log_n, T, B):
+    """The roofline of the metric op as a whole (NTT + Hadamard + INTT, three
+    launches; the target is stated on it) with the per-kernel figures under
+    "kernels".  HBM: algorithmic bytes (24 B per coefficient)
+    over the launch-stream event time of the timed steps.  VALU: the measured
+    VALU instructions per coefficient (SQ_INSTS_VALU, profiles/pmc_current.json,
+    same build and configuration) at the measured clock and the 0.25 wave64
+    instructions per SIMD per cycle issue ceiling give the pipeline's VALU-bound
+    time; its ratio to the measured time is the VALU fraction.  `bound` is the
+    roof the counters put closer (the larger fraction)."""
+    pm, why = load_pmc(log_n, T, B)
+    pk = (pm or {}).get("kernels", {})
+    kernels = {}
+    valu_ms_total, valu_ok, traffic_total = 0.0, bool(pk), 0.0
+    for name, ms in kernels_ms.items():
+        alg = KERNEL_BYTES[name] * coeffs_rank
+        ent = {"ms": ms, "alg_bytes": alg, "achieved_gbs": alg / (ms * 1e-3) / 1e9,
+               "hbm_frac": alg / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, "traffic": None, "valu": None}
+        p = pk.get(name)
+        if p:
+            ent["traffic"] = p.get("hbm_bytes_per_launch")
+            if ent["traffic"] is not None:
+                traffic_total += ent["traffic"]
+            ipc = p.get("valu_insts_per_coeff")
+            clk = p.get("clock_ghz")
+            if ipc and clk:
+                vms = ipc * coeffs_rank / 64 / (SIMDS * clk * 1e9 * VALU_ISSUE_CEILING) * 1e3
+                ent["valu"] = {"lane_insts_per_coeff": ipc, "clock_ghz": clk, "valu_bound_ms": vms,
+                               "valu_frac": vms / ms}
+                valu_ms_total += vms
+            else:
+                valu_ok = False
+        else:
+            valu_ok = False
+        kernels[name] = ent
+    alg = ALG_BYTES_PER_COEFF * coeffs_rank
+    achieved = alg / (pipe_ms * 1e-3) / 1e9
+    hbm_frac = achieved / HBM_PEAK_GBS
+    valu = None
+    if valu_ok and valu_ms_total > 0:
+        valu = {"valu_bound_ms": valu_ms_total, "frac": valu_ms_total / pipe_ms,
+                "lane_insts_per_coeff": sum(kernels[k]["valu"]["lane_insts_per_coeff"] for k in kernels),
+                "issue_ceiling": VALU_ISSUE_CEILING, "simds": SIMDS,
+                "source": "profiles/pmc_current.json (tools/pmc_round.sh, SQ_INSTS_VALU + GRBM_GUI_ACTIVE)"}
+    bound = ("valu" if valu["frac"] > hbm_frac else "hbm") if valu else None
+    dominant = max(kernels_ms, key=kernels_ms.get)
+    return {"bound": bound, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": hbm_frac,
+            "traffic": traffic_total if (pk and all(kernels[k]["traffic"] for k in kernels)) else None,
+            "scope": "pipeline: c = INTT(NTT(a) (.) b), 3 launches (forward column pass, fused block pass, "
+                     "inverse column pass); per-kernel figures under kernels",
+            "alg_bytes_per_step": alg, "ms_per_step_events": pipe_ms, "dominant_kernel": dominant,
+            "valu": valu, "kernels": kernels, "counters": "matched" if pm else why}
+
+
+# ---------------------------------------------------------------------------
+# configs[3]: 32 towers split into contiguous ranges over the ranks (strong scaling)
+# ---------------------------------------------------------------------------
+def bench_configs3(args, ctx, world, rank, dev):
+    import torch
+    import torch.distributed as dist
+
+    import ofhe_hip as H
+    import shard
+
+    log_n, T_total, B = 16, args.c3_towers, args.c3_batch
+    t0, T = shard.shard_towers(T_total, rank, world)
+    n = 1 << log_n
+    qs, roots = moduli_chain(log_n, T_total)
+    plan = H.NTTPlan(ctx, log_n, qs[t0:t0 + T], roots[t0:t0 + T])
+    stream = torch.cuda.current_stream(dev)
+    sp = stream.cuda_stream
+    a = torch.empty((B, T, n), dtype=torch.int64, device=dev)
+    b = torch.empty_like(a)
+    plan.fill_uniform(a.data_ptr(), B, 3, 0, sp)
+    plan.fill_uniform(b.data_ptr(), B, 4, 0, sp)
+    c = torch.empty_like(a)
+
+    def step():
+        plan.ntt_mul_intt(a.data_ptr(), b.data_ptr(), c.data_ptr(), B, sp)
+
+    steps = max(3, args.steps // 2)
+    elapsed, ev_ms = _timed(step, steps, 2, stream, world, dev)
+    del a, b, c
+    plan.close()
+    torch.cuda.empty_cache()
+    if world > 1:
+        dist.barrier()
+    total = B * T_total * n
+    return {"workload": f"configs[3]: N=2^16, {T_total} towers split over {world} GPU(s) "
+                        f"({T} on rank 0), batch {B}, c = INTT(NTT(a) (.) b)",
+            "value": total * steps / elapsed, "unit": "coeffs/s", "scaling": "strong", "steps": steps,
+            "ms_per_step": elapsed / steps * 1e3, "hbm_frac_per_gpu": total / world * 24 / (elapsed / steps) / 8e12,
+            "towers_per_rank": T}
+
+
+# ---------------------------------------------------------------------------
+# configs[4]: HYBRID key switching, N = 2^17, Q = 48, P = 16, dnum = 3
+# ---------------------------------------------------------------------------
+def bench_keyswitch(args, ctx, world, rank, dev, steps, warmup, with_stages=False):
+    import torch
+    import torch.distributed as dist
+
+    import ofhe_hip as H
+    import shard
+
+    log_n, sq, sp_, dnum = 17, 48, 16, 3
+    n = 1 << log_n
+    allq, allr = moduli_chain(log_n, sq + sp_)
+    q, rq, p, rp = allq[:sq], allr[:sq], allq[sq:], allr[sq:]
+    B = args.ks_batch
+    ks = H.KeySwitch(ctx, log_n, q, rq, p, rp, dnum)
+    _, beta = ks.digits(sq)
+    pq = H.NTTPlan(ctx, log_n, q, rq)
+    pqp = H.NTTPlan(ctx, log_n, q + p, rq + rp)
+    stream = torch.cuda.current_stream(dev)
+    sptr = stream.cuda_stream
+    b0, _ = shard.shard_batch(B * world, rank, world)
+    c = torch.empty((B, sq, n), dtype=torch.int64, device=dev)
+    pq.fill_uniform(c.data_ptr(), B, 5, b0, sptr)
+    kb = torch.empty((dnum, sq + sp_, n), dtype=torch.int64, device=dev)
+    ka = torch.empty_like(kb)
+    pqp.fill_uniform(kb.data_ptr(), dnum, 6, 0, sptr)
+    pqp.fill_uniform(ka.data_ptr(), dnum, 7, 0, sptr)
+    key_bcast, comm = None, None
+    if world > 1:  # the evaluation key comes from rank 0 over RCCL (configs[3]/[4])
+        bfn, backend, comm = shard.key_broadcaster(ctx, rank, world)
+        bfn(kb, 0)
+        bfn(ka, 0)
+        key_bcast = {"backend": backend, "verified": shard.same_on_all_ranks(kb) and shard.same_on_all_ranks(ka)}
+    o0 = torch.empty((B, sq, n), dtype=torch.int64, device=dev)
+    o1 = torch.empty_like(o0)
+
+    def step():
+        ks.core(sq, c.data_ptr(), kb.data_ptr(), ka.data_ptr(), o0.data_ptr(), o1.data_ptr(), 0, B, sptr)
+
+    elapsed, ev_ms = _timed(step, steps, warmup, stream, world, dev)
+    stages = None
+    if with_stages:
+        digits = torch.empty((B, beta, sq + sp_, n), dtype=torch.int64, device=dev)
+        ct = torch.empty((2, B, sq + sp_, n), dtype=torch.int64, device=dev)
+        stages = {}
+        reps = max(2, min(steps, 5))
+        calls = {
+            "mod_up(precompute)": lambda: ks.precompute(sq, c.data_ptr(), digits.data_ptr(), B, sptr),
+            "inner_product": lambda: ks.fast_core_ext(sq, digits.data_ptr(), kb.data_ptr(), ka.data_ptr(),
+                                                      ct[0].data_ptr(), ct[1].data_ptr(), B, sptr),
+            "mod_down(x2)": lambda: (ks.mod_down(sq, ct[0].data_ptr(), o0.data_ptr(), 0, B, sptr),
+                                     ks.mod_down(sq, ct[1].data_ptr(), o1.data_ptr(), 0, B, sptr)),
+        }
+        for name, fn in calls.items():
+            fn()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            for _ in range(reps):
+                fn()
+            e1.record(stream)
+            e1.synchronize()
+            stages[name] = e0.elapsed_time(e1) / reps
+        del digits, ct
+    # minimum HBM words per ciphertext polynomial and tower-coefficient: read c
+    # (Q), write + read the digits (2 beta (Q+P)), write ct0/ct1 (2 (Q+P)),
+    # ModDown reads them (2 (Q+P)) and writes out0/out1 (2 Q); keys are shared
+    # by the batch and not counted (DESIGN.md)
+    qp = sq + sp_
+    alg_words = sq + 2 * beta * qp + 4 * qp + 2 * sq
+    if comm is not None:
+        torch.cuda.synchronize()
+        comm.close()
+    del c, kb, ka, o0, o1
+    ks.close()
+    pq.close()
+    pqp.close()
+    torch.cuda.empty_cache()
+    if world > 1:
+        dist.barrier()
+    return {"metric": "HYBRID key switches/sec (KeySwitchCore), N=2^17, 48+16 towers, dnum=3",
+            "value": B * world * steps / elapsed, "unit": "keyswitch/s", "steps": steps, "warmup": warmup,
+            "ms_per_step": elapsed / steps * 1e3, "ms_per_step_events": ev_ms, "scaling": "weak",
+            "config": {"workload": "configs[4]: N=2^17, Q=48, P=16, dnum=3, KeySwitchCore",
+                       "batch_per_gpu": B, "global_batch": B * world,
+                       "parallelism": f"ciphertext-batch-sharded x{world}, key broadcast over RCCL"},
+            "alg_hbm_gbs": alg_words * 8 * n * B / (elapsed / steps) / 1e9, "stages_ms": stages,
+            "evalkey_broadcast": key_bcast}
+
+
+def bench_keyswitch_main(args):
+    """--workload keyswitch: configs[4] as the main JSON line (with the stage split)."""
+    import torch
+    import torch.distributed as dist
+
+    world, rank, local, dev = _dist_setup()
+    import ofhe_hip as H
+
+    ctx = H.Context(local)
+    out = bench_keyswitch(args, ctx, world, rank, dev, steps=args.steps, warmup=args.warmup, with_stages=True)
+    if rank == 0:
+        out.update({"n_gpus": world, "higher_is_better": True, "vs_baseline": None, "dtype": "u64",
+                    "data": "synthetic: splitmix64 ciphertext and key residues (SURVEY.md §8(d) seeds)"})
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+# ---------------------------------------------------------------------------
+# configs[0]: CPU-only poly benchmark, N = 2^14, 2 towers, POLY_NUM = 2
+# ---------------------------------------------------------------------------
+def bench_configs0(ctx):
+    """DCRT_add / DCRT_mul of two evaluation-form DCRTPolys (poly-benchmark-16k.cpp:
+    195-222: c = a->Plus(*b), c = a->Times(*b)), N = 2^14, 2 towers, on the CPU
+    oracle (one thread, as the reference's benchmark loop runs) and, for
+    comparison, one launch of the backend's ModAdd / ModMul on the GPU."""
+    import numpy as np
     import torch
 
-    T, n = a.shape[1], a.shape[2]
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+
+    import ofhe_hip as H
+
+    log_n, T = 14, 2
+    n = 1 << log_n
+    q, r = moduli_chain(log_n, T)
+    a, b = O.uniform_dcrt(1, T, n, q, 1), O.uniform_dcrt(1, T, n, q, 2)
+
+    def per_op(fn, budget=0.5):
+        fn()
+        k, t0 = 0, time.perf_counter()
+        while time.perf_counter() - t0 < budget:
+            fn()
+            k += 1
+        return (time.perf_counter() - t0) / k * 1e6
+
+    threads = int(O.lib().oracle_num_threads())
+    O.lib().oracle_set_threads(1)
+    try:
+        cpu = {"dcrt_add_us": per_op(lambda: O.eltwise("add", a, b, q)),
+               "dcrt_mul_us": per_op(lambda: O.eltwise("mul", a, b, q))}
+    finally:
+        O.lib().oracle_set_threads(threads)
+    plan = H.NTTPlan(ctx, log_n, q, r)
+    da = torch.from_numpy(a.view(np.int64)).cuda()
+    db = torch.from_numpy(b.view(np.int64)).cuda()
+    dc = torch.empty_like(da)
+    s = torch.cuda.current_stream()
+    gpu = {}
+    for name, fn in (("dcrt_add_us", plan.mod_add), ("dcrt_mul_us", plan.mod_mul)):
+        fn(da.data_ptr(), db.data_ptr(), dc.data_ptr(), 1, s.cuda_stream)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(s)
+        for _ in range(50):
+            fn(da.data_ptr(), db.data_ptr(), dc.data_ptr(), 1, s.cuda_stream)
+        e1.record(s)
+        e1.synchronize()
+        gpu[name] = e0.elapsed_time(e1) / 50 * 1e3
+    ok = bool(np.array_equal(dc.cpu().numpy().view(np.uint64), O.eltwise("mul", a, b, q)))
+    plan.close()
+    return {"workload": "configs[0]: N=2^14, towers=2, POLY_NUM=2, DCRT_add / DCRT_mul (evaluation form), "
+                        "poly-benchmark-16k.cpp:195-222 semantics",
+            "cpu_port_1thread": cpu, "gpu_one_launch": gpu, "gpu_matches_oracle": ok,
+            "note": "CPU = the oracle's restatement (oracle/ofhe_oracle.c), the reference being unbuildable here; "
+                    "GPU figures are single launches of 2^15 words, launch-latency bound"}
+
+
+# ---------------------------------------------------------------------------
+# CPU baseline: the oracle on the host cores (a bounded sample)
+# ---------------------------------------------------------------------------
+def host_cpu():
+    """(physical cores available to this process, CPU model) from lscpu."""
+    model, cores_per_socket, sockets, tpc = None, None, None, 1
+    try:
+        out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
+        for line in out.splitlines():
+            k, _, v = line.partition(":")
+            v = v.strip()
+            if k.strip() == "Model name":
+                model = v
+            elif k.strip() == "Core(s) per socket":
+                cores_per_socket = int(v)
+            elif k.strip() == "Socket(s)":
+                sockets = int(v)
+            elif k.strip() == "Thread(s) per core":
+                tpc = int(v)
+    except Exception:  # noqa: BLE001
+        pass
+    avail = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    phys = cores_per_socket * sockets if cores_per_socket and sockets else avail
+    cap = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or avail
+    # one thread per physical core among the CPUs this process may use, within OMP_NUM_THREADS
+    cores = max(1, min(cap, avail // max(1, tpc), phys))
+    return cores, model, phys, tpc
+
+
+def cpu_baseline(args, qs, roots, log_n, T):
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+
+    n = 1 << log_n
+    cores, model, phys, tpc = host_cpu()
+    tbs = O.Tables(n, qs, roots)
+    # single thread, one polynomial of all towers (the reference's 41.1 ms figure)
+    O.lib().oracle_set_threads(1)
+    a1, b1 = O.uniform_dcrt(1, T, n, qs, 1), O.uniform_dcrt(1, T, n, qs, 2)
+    O.ntt_mul_intt(a1, b1, tbs)
+    best = 1e9
+    for _ in range(3):
+        t0 = time.perf_counter()
+        O.ntt_mul_intt(a1, b1, tbs)
+        best = min(best, time.perf_counter() - t0)
+    one_ms = best * 1e3
+    # all physical cores, OpenMP over batch x towers
+    O.lib().oracle_set_threads(cores)
+    Bs = 4
+    ca, cb = O.uniform_dcrt(Bs, T, n, qs, 1), O.uniform_dcrt(Bs, T, n, qs, 2)
+    O.ntt_mul_intt(ca, cb, tbs)
+    runs, t0 = 0, time.perf_counter()
+    while True:
+        O.ntt_mul_intt(ca, cb, tbs)
+        runs += 1
+        el = time.perf_counter() - t0
+        if el >= args.cpu_seconds:
+            break
+    return {"value": runs * Bs * T * n / el, "unit": "coeffs/s", "cores": cores, "kind": "port",
+            "sample": f"{runs} runs x {Bs} polys x {T} towers x N=2^{log_n} ({el:.1f} s), "
+                      f"oracle/ofhe_oracle.c, OpenMP over batch x towers on {cores} threads",
+            "cpu_model": model, "physical_cores_reported": phys, "threads_per_core": tpc,
+            "host": socket.gethostname(),
+            "single_thread_ms_per_poly": one_ms, "single_thread_coeffs_per_s": T * n / (one_ms * 1e-3),
+            "reference_single_thread_ms_per_poly": REF_CPU_MS_1T,
+            "port_vs_reference_1thread": one_ms / REF_CPU_MS_1T,
+            "note": "the reference's own 41.1 ms (SURVEY.md §6) was measured on the survey container's CPU; "
+                    "the reference is unbuildable here (DESIGN.md (c)), so the port is what runs"}
+
+
+# ---------------------------------------------------------------------------
+# PCIe-inclusive rate (never `value`)
+# ---------------------------------------------------------------------------
+def pcie_inclusive(plan, bc, chunks, dev):
+    """c = INTT(NTT(a) (.) b) with a, b in pinned host memory and c returned to
+    it: chunk i's H2D, chunk i-1's pipeline and chunk i-2's D2H overlap on three
+    streams over two device slots.  Returns coefficients/s over `chunks` chunks
+    of `bc` polynomials."""
+    import torch
+
+    T, n = plan.towers, plan.n
+    a = torch.empty((2 * bc, T, n), dtype=torch.int64, device=dev)
+    b = torch.empty_like(a)
+    c = torch.empty_like(a)
     ha, hb, hc = (torch.empty((bc, T, n), dtype=torch.int64, pin_memory=True) for _ in range(3))
+    sp = torch.cuda.current_stream(dev).cuda_stream
+    plan.fill_uniform(a.data_ptr(), bc, 1, 0, sp)
+    plan.fill_uniform(b.data_ptr(), bc, 2, 0, sp)
     ha.copy_(a[:bc])
     hb.copy_(b[:bc])
     s_in, s_run, s_out = (torch.cuda.Stream(dev) for _ in range(3))
@@ -358,133 +789,16 @@ def pcie_inclusive(plan, a, b, c, bc, chunks, dev):
             ev["out"][sl].record(s_out)
         torch.cuda.synchronize(dev)
 
-    go()  # warm (first pinned transfers, plan tables)
+    go()  # warm (first pinned transfers)
     t0 = time.perf_counter()
     go()
     el = time.perf_counter() - t0
     coeffs = chunks * bc * T * n
+    del a, b, c
+    torch.cuda.empty_cache()
     return {"value": coeffs / el, "unit": "coeffs/s", "chunk_batch": bc, "chunks": chunks,
             "pcie_bytes_per_coeff": 24, "pcie_gbs": coeffs * 24 / el / 1e9,
             "note": "a, b pinned host -> HBM, pipeline, c -> pinned host; 3 streams, double-buffered"}
-
-
-def bench_keyswitch(args):
-    """configs[4]: N = 2^17, 48 Q towers, dnum = 3, P = 16 towers; KeySwitchCore
-    (ModUp -> key inner product -> 2x ModDown) on a batch of ciphertext
-    polynomials per GPU, weak-scaled by batch.  Prints one JSON line."""
-    import torch
-    import torch.distributed as dist
-
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local)
-    torch.cuda.set_device(dev)
-    import ofhe_hip as H
-    import shard
-
-    log_n, sq, sp, dnum = 17, 48, 16, 3
-    n = 1 << log_n
-    allq, allr = moduli_chain(log_n, sq + sp)
-    q, rq, p, rp = allq[:sq], allr[:sq], allq[sq:], allr[sq:]
-    B = args.ks_batch
-    ctx = H.Context(local)
-    ks = H.KeySwitch(ctx, log_n, q, rq, p, rp, dnum)
-    _, beta = ks.digits(sq)
-    g = torch.Generator(device=dev)
-    g.manual_seed(0x5EED + rank)
-
-    def uniform(shape, moduli):
-        x = torch.empty(shape, dtype=torch.int64, device=dev)
-        for t, m in enumerate(moduli):
-            x[..., t, :].random_(0, m, generator=g)
-        return x
-
-    c = uniform((B, sq, n), q)
-    kb = torch.empty((dnum, sq + sp, n), dtype=torch.int64, device=dev)
-    ka = torch.empty_like(kb)
-    if rank == 0 or world == 1:
-        kb.copy_(uniform((dnum, sq + sp, n), q + p))
-        ka.copy_(uniform((dnum, sq + sp, n), q + p))
-    key_bcast, comm = None, None
-    if world > 1:  # the evaluation key comes from rank 0 over RCCL (configs[3]/[4])
-        bfn, backend, comm = shard.key_broadcaster(ctx, rank, world)
-        bfn(kb, 0)
-        bfn(ka, 0)
-        key_bcast = {"backend": backend, "verified": shard.same_on_all_ranks(kb) and shard.same_on_all_ranks(ka)}
-    o0 = torch.empty((B, sq, n), dtype=torch.int64, device=dev)
-    o1 = torch.empty_like(o0)
-    digits = torch.empty((B, beta, sq + sp, n), dtype=torch.int64, device=dev)
-    ct = torch.empty((2, B, sq + sp, n), dtype=torch.int64, device=dev)
-    st = torch.cuda.current_stream(dev)
-    sptr = st.cuda_stream
-
-    def step():
-        ks.core(sq, c.data_ptr(), kb.data_ptr(), ka.data_ptr(), o0.data_ptr(), o1.data_ptr(), 0, B, sptr)
-
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        elapsed = shard.max_over_ranks(elapsed, device=dev)
-    # stage split with events on the launch stream
-    stages = {}
-    reps = max(2, min(args.steps, 5))
-    calls = {
-        "mod_up(precompute)": lambda: ks.precompute(sq, c.data_ptr(), digits.data_ptr(), B, sptr),
-        "inner_product": lambda: ks.fast_core_ext(sq, digits.data_ptr(), kb.data_ptr(), ka.data_ptr(),
-                                                  ct[0].data_ptr(), ct[1].data_ptr(), B, sptr),
-        "mod_down(x2)": lambda: (ks.mod_down(sq, ct[0].data_ptr(), o0.data_ptr(), 0, B, sptr),
-                                 ks.mod_down(sq, ct[1].data_ptr(), o1.data_ptr(), 0, B, sptr)),
-    }
-    for name, fn in calls.items():
-        fn()
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record(st)
-        for _ in range(reps):
-            fn()
-        e1.record(st)
-        e1.synchronize()
-        stages[name] = e0.elapsed_time(e1) / reps
-    # minimum HBM words per ciphertext polynomial and tower-coefficient: read c
-    # (Q), write + read the digits (2 beta (Q+P)), write ct0/ct1 (2 (Q+P)),
-    # ModDown reads them (2 (Q+P)) and writes out0/out1 (2 Q); keys are shared
-    # by the batch and not counted (DESIGN.md)
-    qp = sq + sp
-    alg_words = sq + 2 * beta * qp + 4 * qp + 2 * sq
-    value = B * world * args.steps / elapsed
-    if rank == 0:
-        out = {
-            "metric": "HYBRID key switches/sec (KeySwitchCore), N=2^17, 48+16 towers, dnum=3",
-            "value": value, "unit": "keyswitch/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
-            "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
-            "vs_baseline": None, "dtype": "u64", "data": "synthetic: uniform ciphertext and key residues",
-            "config": {"workload": "configs[4]: N=2^17, Q=48, P=16, dnum=3, KeySwitchCore",
-                       "batch_per_gpu": B, "global_batch": B * world,
-                       "parallelism": f"ciphertext-batch-sharded x{world}, key broadcast over RCCL"},
-            "stages_ms": stages,
-            "alg_hbm_gbs": alg_words * 8 * n * B / (elapsed / args.steps) / 1e9,
-            "evalkey_broadcast": key_bcast,
-        }
-        print(json.dumps(out), flush=True)
-    if world > 1:
-        torch.cuda.synchronize()
-        if comm is not None:
-            comm.close()
-        dist.barrier()
-        dist.destroy_process_group()
 
 
 if __name__ == "__main__":

@@ -486,6 +486,14 @@ u64 oracle_fnv64(const u64* x, u64 n) {
     return h;
 }
 
+void oracle_set_threads(int n) {
+#ifdef _OPENMP
+    omp_set_num_threads(n > 0 ? n : 1);
+#else
+    (void)n;
+#endif
+}
+
 int oracle_num_threads(void) {
 #ifdef _OPENMP
     return omp_get_max_threads();

@@ -68,6 +68,7 @@ def lib() -> ctypes.CDLL:
             "oracle_fill_uniform": (None, [_u64p, _u64, _u64, _u64p]),
             "oracle_fnv64": (_u64, [_u64p, _u64]),
             "oracle_num_threads": (ctypes.c_int, []),
+            "oracle_set_threads": (None, [ctypes.c_int]),
         }
         for name, (res, args) in sig.items():
             f = getattr(L, name)

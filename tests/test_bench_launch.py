@@ -1,0 +1,68 @@
+"""CPU checks of bench.py's launch contract and roofline bookkeeping (no GPU):
+--gpus N starts N ranks itself (torch.distributed.run, gloo for the check),
+WORLD_SIZE disagreeing with --gpus is an error, and the roofline object uses
+PMC counters only when they measured this build and configuration."""
+import json
+import os
+import subprocess
+import sys
+
+from conftest import ROOT
+
+BENCH = os.path.join(ROOT, "bench.py")
+
+
+def _env():
+    env = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    return env
+
+
+def test_gpus_flag_starts_that_many_ranks():
+    r = subprocess.run([sys.executable, BENCH, "--gpus", "2", "--launch-check"], capture_output=True, text=True,
+                       timeout=240, env=_env())
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(line) == 1, r.stdout
+    out = json.loads(line[0])
+    assert out["n_gpus"] == 2 and sorted(out["ranks"]) == [0, 1] and sorted(out["local_ranks"]) == [0, 1]
+    assert len(set(out["pids"])) == 2
+
+
+def test_world_size_mismatch_is_an_error():
+    env = dict(_env(), WORLD_SIZE="3", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, BENCH, "--gpus", "2"], capture_output=True, text=True, timeout=120, env=env)
+    assert r.returncode == 2
+    assert "must agree" in r.stderr
+
+
+def test_roofline_uses_only_matching_counters(tmp_path, monkeypatch):
+    import bench
+
+    kms = {"colpass<fwd>": 3.2, "k_block<fused>": 6.8, "colpass<inv>": 3.4}
+    coeffs = 1024 * 16 * 65536
+    monkeypatch.setattr(bench, "PMC_FILE", str(tmp_path / "none.json"))
+    r = bench.make_roofline(13.5, kms, coeffs, 16, 16, 1024)
+    assert r["bound"] is None and r["valu"] is None and r["traffic"] is None
+    assert abs(r["frac"] - 24 * coeffs / 13.5e-3 / 8e12) < 1e-9
+    assert r["dominant_kernel"] == "k_block<fused>"
+    pm = {"build_id": bench.build_id(), "config": {"log_n": 16, "towers": 16, "batch": 1024},
+          "kernels": {k: {"hbm_bytes_per_launch": bench.KERNEL_BYTES[k] * coeffs, "valu_insts_per_coeff": ipc,
+                          "clock_ghz": 1.6} for k, ipc in zip(kms, (86, 181, 98))}}
+    f = tmp_path / "pmc.json"
+    f.write_text(json.dumps(pm))
+    monkeypatch.setattr(bench, "PMC_FILE", str(f))
+    r = bench.make_roofline(13.5, kms, coeffs, 16, 16, 1024)
+    assert r["counters"] == "matched" and r["bound"] == "valu"
+    assert r["traffic"] == sum(bench.KERNEL_BYTES[k] * coeffs for k in kms)
+    want = (86 + 181 + 98) * coeffs / 64 / (1024 * 1.6e9 * 0.25) * 1e3
+    assert abs(r["valu"]["valu_bound_ms"] - want) < 1e-9
+    pm["build_id"] = "stale"
+    f.write_text(json.dumps(pm))
+    r = bench.make_roofline(13.5, kms, coeffs, 16, 16, 1024)
+    assert r["valu"] is None and "stale" in r["counters"]
+    pm["build_id"] = bench.build_id()
+    pm["config"]["batch"] = 256
+    f.write_text(json.dumps(pm))
+    assert bench.make_roofline(13.5, kms, coeffs, 16, 16, 1024)["valu"] is None

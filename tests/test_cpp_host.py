@@ -17,3 +17,56 @@ def test_cpp_adapter_suite():
     print(r.stdout)
     assert r.returncode == 0, r.stdout + r.stderr
     assert " 0 failures" in r.stdout
+
+
+def _read_chain(path):
+    import numpy as np
+
+    raw = open(path, "rb").read()
+    out, off = [], 0
+    while off < len(raw):
+        n = int(np.frombuffer(raw, np.uint64, 1, off)[0])
+        out.append(np.frombuffer(raw, np.uint64, n, off + 8).copy())
+        off += 8 + 8 * n
+    return out
+
+
+def test_cpp_device_resident_chain(tmp_path):
+    """tests/cpp/chain.cpp strings SwitchFormat -> Times -> SwitchFormat ->
+    scalar Plus/Minus -> ApproxModUp -> KeySwitchCore -> ApproxModDown together
+    on device-resident DCRTPolyHip objects (no host round trip between steps)
+    and dumps every intermediate; each is checked here against the oracle."""
+    import numpy as np
+
+    import keyswitch as K
+    import oracle as O
+
+    d = os.path.join(ROOT, "tests", "cpp")
+    subprocess.run(["make", "-s", "-C", d], check=True)
+    out = str(tmp_path / "chain.bin")
+    r = subprocess.run([os.path.join(d, "chain_bin"), out, "5"], capture_output=True, text=True, timeout=300)
+    print(r.stdout)
+    assert r.returncode == 0, r.stdout + r.stderr
+    v = _read_chain(out)
+    log_n, B, sq, sp, dnum = (int(x) for x in v[0])
+    q, p, rq, rp = ([int(x) for x in a] for a in v[1:5])
+    n = 1 << log_n
+    a, b = v[5].reshape(B, sq, n), v[6].reshape(B, sq, n)
+    kb, ka = v[7].reshape(dnum, sq + sp, n), v[8].reshape(dnum, sq + sp, n)
+    s1, s2 = [int(x) for x in v[9]], [int(x) for x in v[10]]
+    Y, Z, Z2, U, K0, K1, D = v[11:18]
+    tq = O.Tables(n, q, rq)
+    y = O.eltwise("mul", O.ntt_fwd(a, tq), b, q)
+    assert np.array_equal(Y.reshape(B, sq, n), y), "SwitchFormat -> Times"
+    z = O.ntt_inv(y, tq)
+    assert np.array_equal(Z.reshape(B, sq, n), z), "SwitchFormat back"
+    assert np.array_equal(z, O.ntt_mul_intt(a, b, tq)), "the fused pipeline is the same op"
+    z2 = O.sub_scalar(O.add_scalar_at(z, 0, s1, q), s2, q)
+    assert np.array_equal(Z2.reshape(B, sq, n), z2), "Plus(Integer) in coefficient form, Minus(Integer)"
+    u = K.approx_mod_up(z2, q, rq, p, rp, eval_form=False)
+    assert np.array_equal(U.reshape(B, sq + sp, n), u), "ApproxModUp"
+    kp = K.KeySwitchParams(n, q, rq, p, rp, dnum)
+    r0, r1 = K.ks_core(kp, y, kb, ka)
+    assert np.array_equal(K0.reshape(B, sq, n), r0), "KeySwitchCore ct0"
+    assert np.array_equal(K1.reshape(B, sq, n), r1), "KeySwitchCore ct1"
+    assert np.array_equal(D.reshape(B, sq, n), O.ntt_fwd(z2, tq)), "ApproxModDown(P * ApproxModUp(z2)) = z2"

@@ -110,6 +110,7 @@ struct ofhe_plan_s {
     bool split8 = false;  // log_n == 16: 8 column stages + 8 block stages (k_tcols + k_block<.,.,2>)
     hipStream_t st[2] = {nullptr, nullptr};
     hipEvent_t ev_fork = nullptr, ev_join[2] = {nullptr, nullptr};
+    std::mutex fork_mu;  // guards st / ev_* (plan_tune, the two-stream pipeline)
 };
 
 struct ofhe_bconv_s {

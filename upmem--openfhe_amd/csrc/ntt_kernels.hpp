@@ -659,16 +659,23 @@ __global__ __launch_bounds__(256, OFHE_KB_WAVES) void k_block(PlanArgs P, const 
 #define OFHE_TCOLS_W 16  // tile width in columns: 16 (128-byte row segments) or 32 (256-byte)
 #endif
 constexpr u32 TCOLS_W = OFHE_TCOLS_W;
+#ifndef OFHE_TCOLS_PADF
+#define OFHE_TCOLS_PADF 1
+#endif
 static_assert(TCOLS_W == 16 || TCOLS_W == 32, "column tile width");
 template <bool INV, bool SPQ>
 __global__ __launch_bounds__(16 * TCOLS_W, OFHE_KB_WAVES) void k_tcols(PlanArgs P, const u64* src, u64* dst,
                                                                        u32 batch, u32 nwg) {
     constexpr u32 N = 1u << 16, S = 256, W = TCOLS_W;
-    // Unpadded tile: both exchange patterns (p = tid + 16W k and p = 16W h +
-    // W k + r) give every LDS lane group contiguous words, so they are bank
-    // conflict free as they stand (a p + p/16 padding made the inverse's
-    // 32-lane ds_read_b64 groups 2-way conflicted).
-    __shared__ u64 lds[16 * 16 * W];
+    // Exchange patterns p = tid + 16W k (round 1) and p = 16W h + W k + r
+    // (round 2).  The inverse writes the second and reads the first: unpadded,
+    // both conflict free (SQ_LDS_BANK_CONFLICT = 0; a p + p/16 padding made its
+    // 32-lane ds_read_b64 groups 2-way conflicted).  The forward READS the
+    // second pattern, where a half-wave's two rows h, h + 1 hit the same 32
+    // banks (2-way, measured 0.56 conflict cycles per active LDS cycle); with
+    // OFHE_TCOLS_PADF it shifts row h by 16 words per 16W-word row
+    // (lds index p + 16 (p / 16W)), so rows h and h + 1 cover all 64 banks.
+    __shared__ u64 lds[16 * 16 * W + 16 * 16];
     const u32 tid = threadIdx.x;
     const u32 wid = xcd_remap(blockIdx.x, nwg);
     const u32 cb = wid % (S / W);
@@ -685,16 +692,17 @@ __global__ __launch_bounds__(16 * TCOLS_W, OFHE_KB_WAVES) void k_tcols(PlanArgs 
     u64 v[16];
     if (!INV) {
         const u64* tw = P.tw + (u64)t * N * 2;
+        constexpr u32 RP = OFHE_TCOLS_PADF ? 16 * W + 16 : 16 * W;  // padded row pitch
         // round 1: rows h + 16k (p = tid + 16W k), stages m = 1..8
 #pragma unroll
         for (int k = 0; k < 16; k++) v[k] = ld_s(x + (u64)(h + 16 * k) * S + r);
         fwd_round16_canon(v, tw, 1, M);
 #pragma unroll
-        for (int k = 0; k < 16; k++) lds[L1 + 16 * W * k] = v[k];
+        for (int k = 0; k < 16; k++) lds[L1 + RP * k] = v[k];
         __syncthreads();
         // round 2: rows 16h + k (p = 16W h + W k + r), stages m = 16..128
 #pragma unroll
-        for (int k = 0; k < 16; k++) v[k] = lds[L2 + W * k];
+        for (int k = 0; k < 16; k++) v[k] = lds[h * RP + r + W * k];
         fwd_round16(v, tw, 16 + h, M);
 #pragma unroll
         for (int k = 0; k < 16; k++) st_s(y + (u64)(16 * h + k) * S + r, v[k]);

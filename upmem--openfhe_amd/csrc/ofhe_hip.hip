@@ -318,12 +318,31 @@ int ofhe_hip_plan_tune(ofhe_plan_t p, uint32_t chunk_batch, uint32_t streams) {
     if (!p || !p->ctx) return fail(OFHE_ERR_STATE, "plan is NULL or destroyed");
     if (streams < 1 || streams > 2) return fail(OFHE_ERR_ARG, "streams must be 1 or 2");
     HIPCHK(hipSetDevice(p->ctx->device));
+    std::lock_guard<std::mutex> lk(p->fork_mu);
     if (streams == 2 && !p->st[0]) {
-        for (int i = 0; i < 2; i++) {
-            HIPCHK(hipStreamCreateWithFlags(&p->st[i], hipStreamNonBlocking));
-            HIPCHK(hipEventCreateWithFlags(&p->ev_join[i], hipEventDisableTiming));
+        // create everything into locals and commit only when all succeeded,
+        // so a failure leaves the plan as it was
+        hipStream_t st[2] = {nullptr, nullptr};
+        hipEvent_t fork = nullptr, join[2] = {nullptr, nullptr};
+        hipError_t e = hipSuccess;
+        for (int i = 0; i < 2 && e == hipSuccess; i++) {
+            e = hipStreamCreateWithFlags(&st[i], hipStreamNonBlocking);
+            if (e == hipSuccess) e = hipEventCreateWithFlags(&join[i], hipEventDisableTiming);
         }
-        HIPCHK(hipEventCreateWithFlags(&p->ev_fork, hipEventDisableTiming));
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&fork, hipEventDisableTiming);
+        if (e != hipSuccess) {
+            for (int i = 0; i < 2; i++) {
+                if (st[i]) (void)hipStreamDestroy(st[i]);
+                if (join[i]) (void)hipEventDestroy(join[i]);
+            }
+            if (fork) (void)hipEventDestroy(fork);
+            return fail(OFHE_ERR_HIP, std::string("plan_tune: ") + hipGetErrorString(e));
+        }
+        for (int i = 0; i < 2; i++) {
+            p->st[i] = st[i];
+            p->ev_join[i] = join[i];
+        }
+        p->ev_fork = fork;
     }
     p->chunk_batch = chunk_batch;
     p->nstreams = streams;
@@ -604,6 +623,10 @@ int ofhe_hip_ntt_mul_intt(ofhe_plan_t p, const uint64_t* a_, const uint64_t* b, 
         const u32 cb = (p->chunk_batch && p->chunk_batch < batch) ? p->chunk_batch : batch;
         const u64 words = (u64)p->towers << p->log_n;
         const bool multi = p->nstreams == 2 && cb < batch;
+        // the fork / join events and side streams are the plan's: one caller at
+        // a time records and waits on them (PlanCache shares plans process-wide)
+        std::unique_lock<std::mutex> lk(p->fork_mu, std::defer_lock);
+        if (multi) lk.lock();
         if (multi) {
             HIPCHK(hipEventRecord(p->ev_fork, s));
             for (int i = 0; i < 2; i++) HIPCHK(hipStreamWaitEvent(p->st[i], p->ev_fork, 0));

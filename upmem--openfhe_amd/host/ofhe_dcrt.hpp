@@ -69,18 +69,16 @@ public:
     }
     ofhe_ctx_t ctx() const { return ctx_; }
     int device() const { return device_; }
+    // Every adapter op runs on one stream (the device's null stream), and
+    // buffers are allocated and released in that stream's order: a DCRTPoly
+    // temporary may die right after the call that reads it -- its memory is
+    // returned only once the queued work has finished, and nothing waits.
     void* allocate(size_t bytes) {
         void* p = nullptr;
-        check(ofhe_hip_alloc(ctx_, bytes, &p), "HipManager::allocate");
+        check(ofhe_hip_alloc_async(ctx_, bytes, &p, nullptr), "HipManager::allocate");
         return p;
     }
-    // A buffer may be dropped while kernels that read it are still queued
-    // (DCRTPoly temporaries die right after the call that uses them): drain
-    // the stream every adapter op uses before releasing it.
-    void deallocate(void* p) {
-        sync();
-        check(ofhe_hip_free(ctx_, p), "HipManager::deallocate");
-    }
+    void deallocate(void* p) { check(ofhe_hip_free_async(ctx_, p, nullptr), "HipManager::deallocate"); }
     void zero(void* dst, size_t bytes) { check(ofhe_hip_zero(ctx_, dst, bytes, nullptr), "HipManager::zero"); }
     // Host <-> device copies of pageable memory are bracketed by stream syncs:
     // HIP may stage them outside the stream's order, and the host buffer may
@@ -123,10 +121,7 @@ public:
         return *this;
     }
     ~DeviceBuffer() {
-        if (p_) {
-            (void)ofhe_hip_sync(m_->ctx(), nullptr);
-            (void)ofhe_hip_free(m_->ctx(), p_);
-        }
+        if (p_) (void)ofhe_hip_free_async(m_->ctx(), p_, nullptr);  // stream-ordered, no wait
     }
     uint64_t* get() const { return p_; }
     size_t size() const { return n_; }
@@ -294,6 +289,11 @@ public:
           buf_(p_->manager(), (size_t)batch * p_->Towers() * p_->GetRingDimension()) {
         buf_.zero();
     }
+    // a result buffer the producing op overwrites entirely: no zero fill
+    struct Uninit {};
+    DCRTPolyHip(std::shared_ptr<DCRTParams> p, Format f, uint32_t batch, Uninit)
+        : p_(std::move(p)), f_(f), batch_(batch),
+          buf_(p_->manager(), (size_t)batch * p_->Towers() * p_->GetRingDimension()) {}
     DCRTPolyHip(const DCRTPolyHip& o) : p_(o.p_), f_(o.f_), batch_(o.batch_), buf_(o.p_->manager(), o.buf_.size()) {
         buf_.copy_from(o.buf_);
     }
@@ -341,30 +341,54 @@ public:
 
     DCRTPolyHip Plus(const DCRTPolyHip& rhs) const {
         check_compat(rhs, "Plus", false);
-        DCRTPolyHip r(p_, f_, batch_);
+        DCRTPolyHip r(p_, f_, batch_, Uninit{});
         check(ofhe_hip_modadd_vv(p_->plan(), data(), rhs.data(), r.data(), batch_, nullptr), "Plus");
         return r;
     }
     DCRTPolyHip Minus(const DCRTPolyHip& rhs) const {
         check_compat(rhs, "Minus", false);
-        DCRTPolyHip r(p_, f_, batch_);
+        DCRTPolyHip r(p_, f_, batch_, Uninit{});
         check(ofhe_hip_modsub_vv(p_->plan(), data(), rhs.data(), r.data(), batch_, nullptr), "Minus");
         return r;
     }
     // Times (dcrtpoly.h:185-200): EVALUATION format only
     DCRTPolyHip Times(const DCRTPolyHip& rhs) const {
         check_compat(rhs, "Times", true);
-        DCRTPolyHip r(p_, f_, batch_);
+        DCRTPolyHip r(p_, f_, batch_, Uninit{});
         check(ofhe_hip_modmul_vv(p_->plan(), data(), rhs.data(), r.data(), batch_, nullptr), "Times");
         return r;
     }
     // Times(const std::vector<NativeInteger>&): one scalar per tower (Shoup)
     DCRTPolyHip Times(const std::vector<uint64_t>& scalars) const {
         if (scalars.size() != p_->Towers()) throw math_error("Times: one scalar per tower required");
-        DCRTPolyHip r(p_, f_, batch_);
+        DCRTPolyHip r(p_, f_, batch_, Uninit{});
         check(ofhe_hip_modmul_scalar(p_->plan(), data(), scalars.data(), r.data(), batch_, nullptr), "Times");
         return r;
     }
+    // Plus / Minus with one integer per tower (dcrtpoly.h:162-163, 182-183;
+    // dcrtpoly-impl.h:545-584).  PolyImpl::Plus(Integer) adds the constant
+    // polynomial: in COEFFICIENT form only coefficient 0 changes
+    // (ModAddAtIndex(0), poly-impl.h:213-220), in EVALUATION form every slot;
+    // PolyImpl::Minus(Integer) subtracts from every word in either form
+    // (poly-impl.h:223-227), as the reference does.
+    DCRTPolyHip Plus(const std::vector<uint64_t>& crt) const {
+        if (crt.size() != p_->Towers()) throw math_error("Plus: one integer per tower required");
+        DCRTPolyHip r(*this);
+        if (f_ == Format::COEFFICIENT)
+            check(ofhe_hip_modadd_scalar_at(p_->plan(), r.data(), 0, crt.data(), r.data(), batch_, nullptr), "Plus");
+        else
+            check(ofhe_hip_modadd_scalar(p_->plan(), data(), crt.data(), r.data(), batch_, nullptr), "Plus");
+        return r;
+    }
+    DCRTPolyHip Minus(const std::vector<uint64_t>& crt) const {
+        if (crt.size() != p_->Towers()) throw math_error("Minus: one integer per tower required");
+        DCRTPolyHip r(p_, f_, batch_, Uninit{});
+        check(ofhe_hip_modsub_scalar(p_->plan(), data(), crt.data(), r.data(), batch_, nullptr), "Minus");
+        return r;
+    }
+    // Plus / Minus(const Integer&): the same integer in every tower
+    DCRTPolyHip Plus(uint64_t v) const { return Plus(std::vector<uint64_t>(p_->Towers(), v)); }
+    DCRTPolyHip Minus(uint64_t v) const { return Minus(std::vector<uint64_t>(p_->Towers(), v)); }
     DCRTPolyHip& operator+=(const DCRTPolyHip& rhs) {
         check_compat(rhs, "operator+=", false);
         check(ofhe_hip_modadd_vv(p_->plan(), data(), rhs.data(), data(), batch_, nullptr), "operator+=");
@@ -390,14 +414,14 @@ public:
         if (f_ != Format::COEFFICIENT || rhs.f_ != Format::EVALUATION)
             throw not_implemented_error("MulViaNTT: needs COEFFICIENT x EVALUATION");
         check_compat(rhs, "MulViaNTT", false, false);
-        DCRTPolyHip r(p_, Format::COEFFICIENT, batch_);
+        DCRTPolyHip r(p_, Format::COEFFICIENT, batch_, Uninit{});
         check(ofhe_hip_ntt_mul_intt(p_->plan(), data(), rhs.data(), r.data(), batch_, nullptr), "MulViaNTT");
         return r;
     }
 
     // AutomorphismTransform(k) (dcrtpoly-impl.h:350-358 -> poly-impl.h:312-365)
     DCRTPolyHip AutomorphismTransform(uint32_t k) const {
-        DCRTPolyHip r(p_, f_, batch_);
+        DCRTPolyHip r(p_, f_, batch_, Uninit{});
         check(ofhe_hip_automorphism(p_->plan(), k, f_ == Format::EVALUATION, data(), r.data(), batch_, nullptr),
               "AutomorphismTransform");
         return r;
@@ -444,7 +468,7 @@ public:
     BaseConverter& operator=(const BaseConverter&) = delete;
     DCRTPolyHip ApproxSwitchCRTBasis(const DCRTPolyHip& x, const std::shared_ptr<DCRTParams>& paramsP) const {
         if (x.GetFormat() != Format::COEFFICIENT) throw math_error("ApproxSwitchCRTBasis: COEFFICIENT form expected");
-        DCRTPolyHip out(paramsP, Format::COEFFICIENT, x.Batch());
+        DCRTPolyHip out(paramsP, Format::COEFFICIENT, x.Batch(), DCRTPolyHip::Uninit{});
         check(ofhe_hip_approx_switch_crt_basis(h_, x.data(), out.data(), x.Batch(), nullptr), "ApproxSwitchCRTBasis");
         return out;
     }
@@ -461,7 +485,7 @@ inline DCRTPolyHip ApproxModUp(const DCRTPolyHip& x, const std::shared_ptr<DCRTP
                                const std::shared_ptr<DCRTParams>& paramsQP, const BaseConverter& q_to_p) {
     const auto& Q = x.GetParams();
     if (paramsQP->Towers() != Q->Towers() + paramsP->Towers()) throw math_error("ApproxModUp: paramsQP size");
-    DCRTPolyHip out(paramsQP, Format::EVALUATION, x.Batch());
+    DCRTPolyHip out(paramsQP, Format::EVALUATION, x.Batch(), DCRTPolyHip::Uninit{});
     check(ofhe_hip_approx_mod_up(Q->plan(), paramsP->plan(), q_to_p.handle(), x.GetFormat() == Format::EVALUATION,
                                  x.data(), out.data(), x.Batch(), nullptr),
           "ApproxModUp");
@@ -476,7 +500,7 @@ inline DCRTPolyHip ApproxModDown(const DCRTPolyHip& x, const std::shared_ptr<DCR
     if (x.GetParams()->Towers() != paramsQ->Towers() + paramsP->Towers())
         throw math_error("ApproxModDown: tower count mismatch");
     if (PInvModq.size() != paramsQ->Towers()) throw math_error("ApproxModDown: PInvModq size");
-    DCRTPolyHip out(paramsQ, Format::EVALUATION, x.Batch());
+    DCRTPolyHip out(paramsQ, Format::EVALUATION, x.Batch(), DCRTPolyHip::Uninit{});
     check(ofhe_hip_approx_mod_down(paramsQ->plan(), paramsP->plan(), p_to_q.handle(), PInvModq.data(), t, x.data(),
                                    out.data(), x.Batch(), nullptr),
           "ApproxModDown");
@@ -514,7 +538,8 @@ public:
         if (key_b.Batch() != numPartQ_ || key_a.Batch() != numPartQ_ ||
             key_b.GetParams()->Towers() != sizeQ_ + sizeP_ || key_a.GetParams()->Towers() != sizeQ_ + sizeP_)
             throw math_error("KeySwitchCore: evaluation key must be numPartQ polynomials over Q|P");
-        DCRTPolyHip o0(c.GetParams(), Format::EVALUATION, c.Batch()), o1(c.GetParams(), Format::EVALUATION, c.Batch());
+        DCRTPolyHip o0(c.GetParams(), Format::EVALUATION, c.Batch(), DCRTPolyHip::Uninit{}),
+            o1(c.GetParams(), Format::EVALUATION, c.Batch(), DCRTPolyHip::Uninit{});
         check(ofhe_hip_ks_core(h_, l, c.data(), key_b.data(), key_a.data(), o0.data(), o1.data(), t, c.Batch(),
                                nullptr),
               "KeySwitchCore");

@@ -79,14 +79,32 @@ def key_broadcaster(ctx, rank: int, world: int):
     """(broadcast function, backend label, communicator or None): the C-ABI
     communicator when it comes up, else torch.distributed's own RCCL group
     (the failure is named).  Close the communicator (comm.close()) before
-    destroying the process group, not at interpreter exit."""
+    destroying the process group, not at interpreter exit.
+
+    The ranks agree on the backend: each reports whether its communicator
+    came up (all_reduce MIN of an ok flag), and unless every rank succeeded
+    they all close theirs and use torch.distributed -- a rank never calls
+    ncclBroadcast while a peer sits in dist.broadcast."""
+    import torch
+    import torch.distributed as dist
+
     import ofhe_hip as H
 
+    comm, err = None, None
     try:
         comm = open_comm(ctx, rank, world)
     except H.MathError as e:
-        return (lambda key, src=0: broadcast_evalkey(key, src)), f"torch.distributed nccl (C-ABI comm: {e})", None
-    return (lambda key, src=0: bcast_evalkey_capi(comm, key, src)), "ofhe_hip_bcast_evalkey (RCCL)", comm
+        err = str(e)
+    backend = dist.get_backend()
+    dev = torch.device("cuda", torch.cuda.current_device()) if backend == "nccl" else torch.device("cpu")
+    ok = torch.tensor([1 if comm is not None else 0], dtype=torch.int32, device=dev)
+    dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+    if int(ok.item()) == 1:
+        return (lambda key, src=0: bcast_evalkey_capi(comm, key, src)), "ofhe_hip_bcast_evalkey (RCCL)", comm
+    if comm is not None:
+        comm.close()
+    why = err if err else "a peer rank's C-ABI communicator failed"
+    return (lambda key, src=0: broadcast_evalkey(key, src)), f"torch.distributed {backend} (C-ABI comm: {why})", None
 
 
 def max_over_ranks(value: float, device=None) -> float:
