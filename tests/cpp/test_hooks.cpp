@@ -1,0 +1,158 @@
+// The RUN_ON_HIP hook bodies (upmem--openfhe_amd/host/ofhe_openfhe_hooks.hpp)
+// instantiated on a tower type with the reference's accessor surface and
+// checked against the CPU oracle (oracle/libofhe_oracle.so, test
+// infrastructure).  The mock below is this repo's own test double written to
+// the reference's method names -- PolyImpl::GetParams() / operator[]
+// (poly.h:209-215), ILNativeParams::GetModulus() / GetRootOfUnity() /
+// GetRingDimension(), NativeIntegerT::ConvertToInt() with one uint64_t member
+// (ubintnat.h:139-141, 1659) -- not a copy of any reference header: it shows
+// that the hooks compile against, and only need, that surface.
+#include <cstdio>
+#include <memory>
+#include <random>
+#include <vector>
+
+#include "../../upmem--openfhe_amd/host/ofhe_openfhe_hooks.hpp"
+
+extern "C" {
+int oracle_moduli_chain(unsigned bits, uint64_t cyclo_order, unsigned count, uint64_t* q_out, uint64_t* psi_out);
+int oracle_ntt_tables(uint64_t n, uint64_t q, uint64_t psi, uint64_t* tab, uint64_t* tab_pre, uint64_t* itab,
+                      uint64_t* itab_pre, uint64_t* coi, uint64_t* coi_pre);
+void oracle_ntt_fwd(uint64_t* x, uint64_t len, uint64_t q, const uint64_t* tab, const uint64_t* tab_pre);
+void oracle_ntt_inv(uint64_t* x, uint64_t n, uint64_t q, const uint64_t* itab, const uint64_t* itab_pre,
+                    uint64_t ninv, uint64_t ninv_pre);
+void oracle_vec_modmul(const uint64_t* a, const uint64_t* b, uint64_t* c, uint64_t n, uint64_t q);
+void oracle_vec_modadd(const uint64_t* a, const uint64_t* b, uint64_t* c, uint64_t n, uint64_t q);
+void oracle_vec_modsub(const uint64_t* a, const uint64_t* b, uint64_t* c, uint64_t n, uint64_t q);
+void oracle_base_conv_precompute(unsigned sizeQ, unsigned sizeP, const uint64_t* q, const uint64_t* p,
+                                 uint64_t* qhatinv_modq, uint64_t* qhatinv_modq_pre, uint64_t* qhat_modp,
+                                 uint64_t* mu_lo, uint64_t* mu_hi);
+void oracle_approx_switch_crt_basis(const uint64_t* x, uint64_t* out, uint64_t n, unsigned sizeQ, unsigned sizeP,
+                                    const uint64_t* q, const uint64_t* p, const uint64_t* qhatinv_modq,
+                                    const uint64_t* qhatinv_modq_pre, const uint64_t* qhat_modp,
+                                    const uint64_t* mu_lo, const uint64_t* mu_hi);
+}
+
+namespace mock {
+struct NativeInteger {  // NativeIntegerT<uint64_t>: one word
+    uint64_t m_value = 0;
+    uint64_t ConvertToInt() const { return m_value; }
+};
+struct ILNativeParams {
+    NativeInteger modulus, root;
+    uint32_t ring;
+    const NativeInteger& GetModulus() const { return modulus; }
+    const NativeInteger& GetRootOfUnity() const { return root; }
+    uint32_t GetRingDimension() const { return ring; }
+};
+struct PolyImpl {
+    std::shared_ptr<ILNativeParams> params;
+    std::vector<NativeInteger> values;
+    const std::shared_ptr<ILNativeParams>& GetParams() const { return params; }
+    NativeInteger& operator[](uint32_t i) { return values[i]; }
+    const NativeInteger& operator[](uint32_t i) const { return values[i]; }
+};
+}  // namespace mock
+
+static int g_fail = 0;
+#define CHECK(c, msg)                                      \
+    do {                                                   \
+        if (!(c)) {                                        \
+            std::printf("  FAIL %s:%d %s\n", __FILE__, __LINE__, msg); \
+            g_fail++;                                      \
+        }                                                  \
+    } while (0)
+
+static std::vector<mock::PolyImpl> towers(uint32_t n, const std::vector<uint64_t>& q, const std::vector<uint64_t>& r,
+                                          std::mt19937_64& rng) {
+    std::vector<mock::PolyImpl> out;
+    for (size_t t = 0; t < q.size(); t++) {
+        auto p = std::make_shared<mock::ILNativeParams>(mock::ILNativeParams{{q[t]}, {r[t]}, n});
+        mock::PolyImpl x{p, std::vector<mock::NativeInteger>(n)};
+        for (auto& v : x.values) v.m_value = rng() % q[t];
+        out.push_back(std::move(x));
+    }
+    return out;
+}
+static std::vector<uint64_t> words(const mock::PolyImpl& p) {
+    std::vector<uint64_t> w;
+    for (auto& v : p.values) w.push_back(v.m_value);
+    return w;
+}
+
+int main() {
+    const uint32_t log_n = 12, n = 1u << log_n, T = 5, P = 3;
+    std::vector<uint64_t> all(T + P), roots(T + P);
+    oracle_moduli_chain(60, 2 * n, T + P, all.data(), roots.data());
+    std::vector<uint64_t> q(all.begin(), all.begin() + T), r(roots.begin(), roots.begin() + T);
+    std::vector<uint64_t> p(all.begin() + T, all.end()), rp(roots.begin() + T, roots.end());
+    std::mt19937_64 rng(77);
+    try {
+        // SwitchFormat both ways, against the oracle's per-tower transforms
+        auto a = towers(n, q, r, rng);
+        auto a0 = a;
+        ofhe::hooks::SwitchFormat(a, true);
+        bool ok = true;
+        for (uint32_t t = 0; t < T; t++) {
+            std::vector<uint64_t> tab(n), tp(n), it(n), ip(n), coi(log_n + 1), cp(log_n + 1), x = words(a0[t]);
+            oracle_ntt_tables(n, q[t], r[t], tab.data(), tp.data(), it.data(), ip.data(), coi.data(), cp.data());
+            oracle_ntt_fwd(x.data(), n, q[t], tab.data(), tp.data());
+            ok = ok && x == words(a[t]);
+        }
+        CHECK(ok, "hooks::SwitchFormat (forward) vs oracle");
+        ofhe::hooks::SwitchFormat(a, false);
+        ok = true;
+        for (uint32_t t = 0; t < T; t++) ok = ok && words(a[t]) == words(a0[t]);
+        CHECK(ok, "hooks::SwitchFormat round trip");
+        // element-wise *=, +=, -= against the oracle
+        auto b = towers(n, q, r, rng);
+        for (int op = 0; op < 3; op++) {
+            auto x = a0;
+            if (op == 0) ofhe::hooks::TimesEq(x, b);
+            if (op == 1) ofhe::hooks::PlusEq(x, b);
+            if (op == 2) ofhe::hooks::MinusEq(x, b);
+            ok = true;
+            for (uint32_t t = 0; t < T; t++) {
+                std::vector<uint64_t> wa = words(a0[t]), wb = words(b[t]), wc(n);
+                (op == 0 ? oracle_vec_modmul : op == 1 ? oracle_vec_modadd : oracle_vec_modsub)(wa.data(), wb.data(),
+                                                                                               wc.data(), n, q[t]);
+                ok = ok && wc == words(x[t]);
+            }
+            CHECK(ok, op == 0 ? "hooks::TimesEq" : op == 1 ? "hooks::PlusEq" : "hooks::MinusEq");
+        }
+        // ApproxSwitchCRTBasis Q -> P against the oracle
+        std::vector<uint64_t> hinv(T), hinvp(T), hmod(T * P), mlo(P), mhi(P);
+        oracle_base_conv_precompute(T, P, q.data(), p.data(), hinv.data(), hinvp.data(), hmod.data(), mlo.data(),
+                                    mhi.data());
+        auto out = towers(n, p, rp, rng);
+        ofhe::hooks::ApproxSwitchCRTBasis(a0, out, hinv, hmod);
+        std::vector<uint64_t> xin, want(P * (size_t)n);
+        for (auto& t : a0) {
+            auto w = words(t);
+            xin.insert(xin.end(), w.begin(), w.end());
+        }
+        oracle_approx_switch_crt_basis(xin.data(), want.data(), n, T, P, q.data(), p.data(), hinv.data(), hinvp.data(),
+                                       hmod.data(), mlo.data(), mhi.data());
+        ok = true;
+        for (uint32_t j = 0; j < P; j++)
+            ok = ok && std::vector<uint64_t>(want.begin() + j * (size_t)n, want.begin() + (j + 1) * (size_t)n) ==
+                           words(out[j]);
+        CHECK(ok, "hooks::ApproxSwitchCRTBasis vs oracle");
+        // the reference's error behaviour: mismatched bases throw math_error
+        bool thrown = false;
+        try {
+            auto x = a0;
+            auto y = towers(n, p, rp, rng);
+            y.resize(x.size(), y[0]);
+            ofhe::hooks::PlusEq(x, y);
+        } catch (const ofhe::math_error&) {
+            thrown = true;
+        }
+        CHECK(thrown, "PlusEq over different moduli throws math_error");
+    } catch (const std::exception& e) {
+        std::printf("  FAIL exception %s\n", e.what());
+        g_fail++;
+    }
+    std::printf("hooks: %d failures\n", g_fail);
+    return g_fail ? 1 : 0;
+}

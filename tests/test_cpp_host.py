@@ -70,3 +70,15 @@ def test_cpp_device_resident_chain(tmp_path):
     assert np.array_equal(K0.reshape(B, sq, n), r0), "KeySwitchCore ct0"
     assert np.array_equal(K1.reshape(B, sq, n), r1), "KeySwitchCore ct1"
     assert np.array_equal(D.reshape(B, sq, n), O.ntt_fwd(z2, tq)), "ApproxModDown(P * ApproxModUp(z2)) = z2"
+
+
+def test_cpp_openfhe_hooks():
+    """The RUN_ON_HIP hook bodies (host/ofhe_openfhe_hooks.hpp) instantiated on a
+    tower type with the reference's accessor names, checked against the oracle
+    (tests/cpp/test_hooks.cpp)."""
+    d = os.path.join(ROOT, "tests", "cpp")
+    subprocess.run(["make", "-s", "-C", d], check=True)
+    r = subprocess.run([os.path.join(d, "test_hooks_bin")], capture_output=True, text=True, timeout=300)
+    print(r.stdout)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "hooks: 0 failures" in r.stdout
