@@ -7,6 +7,7 @@
 #include <functional>
 #include <random>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../upmem--openfhe_amd/host/ofhe_dcrt.hpp"
@@ -396,6 +397,49 @@ int main() {
         auto C = params(m, std::vector<uint64_t>(q.begin(), q.begin() + 2));
         EXPECT_EQ(A->plan() == B->plan(), true, "same basis, same plan");
         EXPECT_EQ(A->plan() == C->plan(), false, "other basis, other plan");
+    });
+    // A tuned plan (chunked batch over the plan's two side streams, whose fork /
+    // join events are shared) driven from four host threads at once, each on
+    // its own stream and data: every result equals the single-thread one.
+    TEST("Plan.concurrent_tuned_pipeline", [] {
+        const uint32_t m = 1u << 14, n = m / 2, T = 3, B = 4;
+        std::vector<uint64_t> q;
+        uint64_t x = first_prime(60, m);
+        for (uint32_t t = 0; t < T; t++) q.push_back(x = previous_prime(x, m));
+        auto P = params(m, q);
+        ofhe_plan_t plan = P->plan();
+        check(ofhe_hip_plan_tune(plan, 1, 2), "tune");
+        HipManager* mg = HipManager::getHip(0);
+        const size_t words = (size_t)B * T * n;
+        std::mt19937_64 rng(31);
+        std::vector<uint64_t> a(words), b(words);
+        for (size_t i = 0; i < words; i++) a[i] = rng() % q[(i / n) % T], b[i] = rng() % q[(i / n) % T];
+        DeviceBuffer da(mg, words), db(mg, words), want(mg, words);
+        da.upload(a.data());
+        db.upload(b.data());
+        check(ofhe_hip_ntt_mul_intt(plan, da.get(), db.get(), want.get(), B, nullptr), "reference run");
+        std::vector<uint64_t> w(words);
+        want.download(w.data());
+        const int NT = 4;
+        std::vector<std::vector<uint64_t>> got(NT, std::vector<uint64_t>(words));
+        std::vector<int> rc(NT, 0);
+        std::vector<std::thread> th;
+        for (int i = 0; i < NT; i++)
+            th.emplace_back([&, i] {
+                void* c = nullptr;
+                rc[i] |= ofhe_hip_alloc(mg->ctx(), words * 8, &c);
+                for (int rep = 0; rep < 5 && !rc[i]; rep++)
+                    rc[i] |= ofhe_hip_ntt_mul_intt(plan, da.get(), db.get(), (uint64_t*)c, B, nullptr);
+                rc[i] |= ofhe_hip_sync(mg->ctx(), nullptr);
+                rc[i] |= ofhe_hip_copy_to_host(mg->ctx(), got[i].data(), c, words * 8, nullptr);
+                rc[i] |= ofhe_hip_sync(mg->ctx(), nullptr);
+                rc[i] |= ofhe_hip_free(mg->ctx(), c);
+            });
+        for (auto& t : th) t.join();
+        bool ok = true;
+        for (int i = 0; i < NT; i++) ok = ok && rc[i] == 0 && got[i] == w;
+        EXPECT_EQ(ok, true, "four threads on one tuned plan");
+        check(ofhe_hip_plan_tune(plan, 0, 1), "untune");
     });
     // Staging: the INTEGRATION.md host-buffer hook.  Towers live in separate
     // host vectors (PolyImpl values); gather into pinned memory, one forward
