@@ -21,6 +21,16 @@
 
 using namespace ofhe;
 
+// A/B switches (tools/exp_ks.py): KeySwitchCore reads each digit's own towers
+// from the ciphertext instead of a copy (OFHE_KS_OWN); ModUp transforms the
+// Q-after-digit and P towers in one launch at full level (OFHE_KS_MERGE).
+#ifndef OFHE_KS_OWN
+#define OFHE_KS_OWN 1
+#endif
+#ifndef OFHE_KS_MERGE
+#define OFHE_KS_MERGE 1
+#endif
+
 namespace {
 
 // prod_{k != skip} ms[k] mod m
@@ -452,14 +462,12 @@ static int ks_check(ofhe_ks_t k, u32 size_ql, u32 batch) {
     return OFHE_OK;
 }
 
-int ofhe_hip_ks_precompute(ofhe_ks_t k, uint32_t size_ql, const uint64_t* c, uint64_t* digits, uint32_t batch,
-                           void* stream) {
-    RCCHK(ks_check(k, size_ql, batch));
-    if (!c || !digits) return fail(OFHE_ERR_ARG, "NULL data pointer");
-    KsLevel* L = nullptr;
-    RCCHK(level_get(k, size_ql, &L));
+// EvalKeySwitchPrecomputeCore; with own_copy = false the digit's own towers
+// are left out of its slot (KeySwitchCore's inner product reads them from c).
+static int ks_precompute_impl(ofhe_ks_t k, KsLevel* L, uint32_t size_ql, const uint64_t* c, uint64_t* digits,
+                              uint32_t batch, hipStream_t stream, bool own_copy) {
     KsFork fk;
-    RCCHK(fk.open(k, pick(stream)));
+    RCCHK(fk.open(k, stream));
     const u64 N = 1ull << k->log_n, l = size_ql, P = k->size_p, poly = (l + P) * N, ds = L->beta * poly;
     for (u32 j = 0; j < L->beta; j++) {
         const u32 st = L->start[j], n = L->cnt[j];
@@ -475,21 +483,36 @@ int ofhe_hip_ks_precompute(ofhe_ks_t k, uint32_t size_ql, const uint64_t* c, uin
         RCCHK(bconv_run(B, slot + st * N, slot, batch, s));
         // complement towers to evaluation form (394)
         RCCHK(plan_ntt_range(k->plan, false, 0, st, slot, slot, ds, ds, batch, s));
-        RCCHK(plan_ntt_range(k->plan, false, st + n, (u32)l - st - n, slot + (st + n) * N, slot + (st + n) * N, ds,
-                             ds, batch, s));
-        RCCHK(plan_ntt_range(k->plan, false, k->size_q, (u32)P, slot + l * N, slot + l * N, ds, ds, batch, s));
+        if (OFHE_KS_MERGE && l == k->size_q) {
+            // full level: the Q towers after the digit and the P towers are
+            // adjacent both in the plan and in the slot -- one launch
+            RCCHK(plan_ntt_range(k->plan, false, st + n, (u32)(l + P) - st - n, slot + (st + n) * N,
+                                 slot + (st + n) * N, ds, ds, batch, s));
+        } else {
+            RCCHK(plan_ntt_range(k->plan, false, st + n, (u32)l - st - n, slot + (st + n) * N, slot + (st + n) * N,
+                                 ds, ds, batch, s));
+            RCCHK(plan_ntt_range(k->plan, false, k->size_q, (u32)P, slot + l * N, slot + l * N, ds, ds, batch, s));
+        }
         // the digit's own towers stay as given (evaluation form, 402-404)
-        RCCHK(copy_rows(slot + st * N, ds, c + st * N, l * N, (u64)n * N, batch, s));
+        if (own_copy) RCCHK(copy_rows(slot + st * N, ds, c + st * N, l * N, (u64)n * N, batch, s));
     }
     return fk.join();
 }
 
-int ofhe_hip_ks_fast_core_ext(ofhe_ks_t k, uint32_t size_ql, const uint64_t* digits, const uint64_t* key_b,
-                              const uint64_t* key_a, uint64_t* ct0, uint64_t* ct1, uint32_t batch, void* stream) {
+int ofhe_hip_ks_precompute(ofhe_ks_t k, uint32_t size_ql, const uint64_t* c, uint64_t* digits, uint32_t batch,
+                           void* stream) {
     RCCHK(ks_check(k, size_ql, batch));
-    if (!digits || !key_b || !key_a || !ct0 || !ct1) return fail(OFHE_ERR_ARG, "NULL data pointer");
+    if (!c || !digits) return fail(OFHE_ERR_ARG, "NULL data pointer");
     KsLevel* L = nullptr;
     RCCHK(level_get(k, size_ql, &L));
+    return ks_precompute_impl(k, L, size_ql, c, digits, batch, pick(stream), true);
+}
+
+// EvalFastKeySwitchCoreExt; c != NULL: the digits' own towers come from c
+// (see ks_precompute_impl), which only the batch-stationary kernel supports.
+static int ks_fast_core_ext_impl(ofhe_ks_t k, KsLevel* L, uint32_t size_ql, const uint64_t* digits,
+                                 const uint64_t* key_b, const uint64_t* key_a, uint64_t* ct0, uint64_t* ct1,
+                                 uint32_t batch, void* stream, const uint64_t* c) {
     const u32 towers = size_ql + k->size_p;
     const u64 key_stride = (u64)(k->size_q + k->size_p) << k->log_n;
     if (L->beta <= 4) {
@@ -497,9 +520,15 @@ int ofhe_hip_ks_fast_core_ext(ofhe_ks_t k, uint32_t size_ql, const uint64_t* dig
         const u64 rows = ((u64)towers << k->log_n) / OFHE_KS_CPT;
         const dim3 g((u32)((rows + 255) / 256)), blk(256);
         hipStream_t s = pick(stream);
+        KsOwn own{};
+        for (u32 j = 0; j < L->beta; j++) {
+            own.start[j] = L->start[j];
+            own.cnt[j] = L->cnt[j];
+        }
+        const u64 c_stride = (u64)size_ql << k->log_n;
 #define OFHE_KS_BS(B_)                                                                                      \
     hipLaunchKernelGGL((k_ks_inner_bs<B_, OFHE_KS_CPT>), g, blk, 0, s, L->d_tow, digits, key_b, key_a, ct0, ct1, \
-                       key_stride, batch, rows, k->log_n, towers)
+                       key_stride, batch, rows, k->log_n, towers, c, c_stride, own)
         switch (L->beta) {
             case 1: OFHE_KS_BS(1); break;
             case 2: OFHE_KS_BS(2); break;
@@ -508,11 +537,21 @@ int ofhe_hip_ks_fast_core_ext(ofhe_ks_t k, uint32_t size_ql, const uint64_t* dig
         }
 #undef OFHE_KS_BS
     } else {
+        if (c) return fail(OFHE_ERR_STATE, "internal: own-tower reads need beta <= 4");
         const u64 npairs = ((u64)batch * towers << k->log_n) / 2;
         hipLaunchKernelGGL(k_ks_inner, dim3(grid_for(npairs)), dim3(256), 0, pick(stream), L->d_tow, digits, key_b,
                            key_a, ct0, ct1, key_stride, L->beta, npairs, k->log_n, towers);
     }
     return post_launch();
+}
+
+int ofhe_hip_ks_fast_core_ext(ofhe_ks_t k, uint32_t size_ql, const uint64_t* digits, const uint64_t* key_b,
+                              const uint64_t* key_a, uint64_t* ct0, uint64_t* ct1, uint32_t batch, void* stream) {
+    RCCHK(ks_check(k, size_ql, batch));
+    if (!digits || !key_b || !key_a || !ct0 || !ct1) return fail(OFHE_ERR_ARG, "NULL data pointer");
+    KsLevel* L = nullptr;
+    RCCHK(level_get(k, size_ql, &L));
+    return ks_fast_core_ext_impl(k, L, size_ql, digits, key_b, key_a, ct0, ct1, batch, stream, nullptr);
 }
 
 static int ks_mod_down_impl(ofhe_ks_t k, KsLevel* L, const u64* x, u64* out, u64 t, u32 batch, hipStream_t s) {
@@ -547,8 +586,11 @@ int ofhe_hip_ks_core(ofhe_ks_t k, uint32_t size_ql, const uint64_t* c, const uin
     RCCHK(ct.alloc((size_t)2 * batch * poly * 8, s));
     u64* c0 = ct.w();
     u64* c1 = ct.w() + (u64)batch * poly;
-    RCCHK(ofhe_hip_ks_precompute(k, size_ql, c, dg.w(), batch, s));
-    RCCHK(ofhe_hip_ks_fast_core_ext(k, size_ql, dg.w(), key_b, key_a, c0, c1, batch, s));
+    // the inner product reads each digit's own towers straight from c (beta <= 4),
+    // so the precompute skips copying them into the digit slots
+    const bool own_from_c = OFHE_KS_OWN && L->beta <= 4;
+    RCCHK(ks_precompute_impl(k, L, size_ql, c, dg.w(), batch, s, !own_from_c));
+    RCCHK(ks_fast_core_ext_impl(k, L, size_ql, dg.w(), key_b, key_a, c0, c1, batch, s, own_from_c ? c : nullptr));
     KsFork fk;  // after dg, ct: joins before they are freed
     RCCHK(fk.open(k, s));
     RCCHK(ks_mod_down_impl(k, L, c0, out0, t, batch, fk.f[0]));

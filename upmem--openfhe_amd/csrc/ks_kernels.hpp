@@ -155,11 +155,20 @@ __device__ __forceinline__ void stw(u64* p, const u64* v) {
     }
 }
 
+// Digit j's own towers [own.start[j], own.start[j] + own.cnt[j]) are the
+// ciphertext's evaluation-form towers unchanged (keyswitch-hybrid.cpp:402-404);
+// when `c` is given they are read from it (c: [batch][size_ql][N], stride
+// c_stride) instead of from a copy in the digit slot, so KeySwitchCore skips
+// writing and re-reading that copy.
+struct KsOwn {
+    u32 start[4], cnt[4];
+};
 template <int BETA, int C>
 __global__ __launch_bounds__(256) void k_ks_inner_bs(const KsTower* __restrict__ tw, const u64* __restrict__ digits,
                                                      const u64* __restrict__ kb, const u64* __restrict__ ka,
                                                      u64* __restrict__ ct0, u64* __restrict__ ct1, u64 key_stride,
-                                                     u32 batch, u64 nthreads, u32 log_n, u32 towers) {
+                                                     u32 batch, u64 nthreads, u32 log_n, u32 towers,
+                                                     const u64* __restrict__ c_in, u64 c_stride, KsOwn own) {
     const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= nthreads) return;
     const u64 e = C * i;
@@ -207,7 +216,10 @@ __global__ __launch_bounds__(256) void k_ks_inner_bs(const KsTower* __restrict__
     auto load = [&](Words<C> (&x)[BETA], u32 b) {
         const u64* d = digits + (u64)b * BETA * poly + inner;
 #pragma unroll
-        for (int j = 0; j < BETA; j++) x[j] = ldw<C>(d + (u64)j * poly);
+        for (int j = 0; j < BETA; j++) {
+            const bool mine = c_in && t - own.start[j] < own.cnt[j];  // wave-uniform for N >= 64 C
+            x[j] = ldw<C>(mine ? c_in + (u64)b * c_stride + inner : d + (u64)j * poly);
+        }
     };
     Words<C> xn[BETA];
     load(xn, 0);
