@@ -76,9 +76,11 @@ int plan_ntt_range(ofhe_plan_t p, bool inverse, u32 t0, u32 count, const u64* sr
 
 // Forward transform of y (towers [t0, t0 + count), in place through the column
 // pass) whose block pass writes out = (x - NTT(y)) * s_t mod q_t instead of
-// NTT(y); scal = device [count][3] (q, s, s').  log_n >= 12.
+// NTT(y); scal = device [count][3] (q, s, s').  log_n >= 12.  parts: 1 = the
+// column pass only, 2 = the block pass only (y already through the column
+// pass), 3 = both.
 int plan_ntt_fwd_sub(ofhe_plan_t p, u32 t0, u32 count, u64* y, u64 ystride, const u64* x, u64 xstride, u64* out,
-                     u64 ostride, const u64* scal, u32 batch, hipStream_t s);
+                     u64 ostride, const u64* scal, u32 batch, hipStream_t s, int parts = 3);
 
 // ApproxSwitchCRTBasis launch (strides and output gap from A)
 int bconv_run(const BconvArgs& A, const u64* x, u64* out, u32 batch, hipStream_t s);

@@ -30,6 +30,11 @@ using namespace ofhe;
 #ifndef OFHE_KS_MERGE
 #define OFHE_KS_MERGE 1
 #endif
+// KeySwitchCore's two ModDowns as one set of launches over 2 x batch
+// (mod_down_run2) instead of two forked streams (OFHE_KS_MD2)
+#ifndef OFHE_KS_MD2
+#define OFHE_KS_MD2 1
+#endif
 
 namespace {
 
@@ -128,6 +133,41 @@ int mod_down_run(const ModDownArgs& A, const u64* x, u64 xstride, u64* out, u64 
                                 reinterpret_cast<const u64*>(A.pinv), batch, s);
     RCCHK(plan_ntt_range(A.plan_q, false, A.q0, A.size_q, sq.w(), sq.w(), qs, qs, batch, s));
     return sub_scale(A.pinv, x, sq.w(), out, xstride, qs, ostride, batch, A.size_q, log_n, s);
+}
+
+// The two ApproxModDowns of KeySwitchCore in one set of launches: ct1
+// follows ct0 in memory (x1 = x0 + batch * xstride), so the P-part INTT, the
+// base conversion and the column pass run once over 2 * batch polynomials;
+// only the block pass, which writes the caller's out0 / out1, runs twice.
+int mod_down_run2(const ModDownArgs& A, const u64* x0, u64 xstride, u64* out0, u64* out1, u64 ostride, u32 batch,
+                  hipStream_t s) {
+    const u32 log_n = A.plan_q->log_n;
+    const u64 N = 1ull << log_n;
+    const u32 b2 = 2 * batch;
+    Scratch sp, sq;
+    RCCHK(sp.alloc((size_t)b2 * A.size_p * N * 8, s));
+    RCCHK(sq.alloc((size_t)b2 * A.size_q * N * 8, s));
+    const u64 ps = A.size_p * N, qs = A.size_q * N;
+    RCCHK(plan_ntt_range(A.plan_p, true, A.p0, A.size_p, x0 + qs, sp.w(), xstride, ps, b2, s));
+    if (A.tinv_p) RCCHK(scale_towers(A.tinv_p, sp.w(), sp.w(), ps, ps, b2, A.size_p, log_n, s));
+    BconvArgs B = A.bconv;
+    B.in_stride = ps;
+    B.out_stride = qs;
+    B.gap_at = A.size_q;
+    B.gap = 0;
+    RCCHK(bconv_run(B, sp.w(), sq.w(), b2, s));
+    if (A.t_q) RCCHK(scale_towers(A.t_q, sq.w(), sq.w(), qs, qs, b2, A.size_q, log_n, s));
+    const u64* x1 = x0 + (u64)batch * xstride;
+    u64* sq1 = sq.w() + (u64)batch * qs;
+    const u64* pinv = reinterpret_cast<const u64*>(A.pinv);
+    if (log_n >= 12) {
+        RCCHK(plan_ntt_fwd_sub(A.plan_q, A.q0, A.size_q, sq.w(), qs, x0, xstride, out0, ostride, pinv, b2, s, 1));
+        RCCHK(plan_ntt_fwd_sub(A.plan_q, A.q0, A.size_q, sq.w(), qs, x0, xstride, out0, ostride, pinv, batch, s, 2));
+        return plan_ntt_fwd_sub(A.plan_q, A.q0, A.size_q, sq1, qs, x1, xstride, out1, ostride, pinv, batch, s, 2);
+    }
+    RCCHK(plan_ntt_range(A.plan_q, false, A.q0, A.size_q, sq.w(), sq.w(), qs, qs, b2, s));
+    RCCHK(sub_scale(A.pinv, x0, sq.w(), out0, xstride, qs, ostride, batch, A.size_q, log_n, s));
+    return sub_scale(A.pinv, x1, sq1, out1, xstride, qs, ostride, batch, A.size_q, log_n, s);
 }
 
 }  // namespace
@@ -591,6 +631,15 @@ int ofhe_hip_ks_core(ofhe_ks_t k, uint32_t size_ql, const uint64_t* c, const uin
     const bool own_from_c = OFHE_KS_OWN && L->beta <= 4;
     RCCHK(ks_precompute_impl(k, L, size_ql, c, dg.w(), batch, s, !own_from_c));
     RCCHK(ks_fast_core_ext_impl(k, L, size_ql, dg.w(), key_b, key_a, c0, c1, batch, s, own_from_c ? c : nullptr));
+    if (OFHE_KS_MD2) {
+        // both ModDowns in one set of launches (c1 = c0 + batch * poly)
+        const TowerScalar* tt = nullptr;
+        if (t) RCCHK(level_t_tables(k, L, t, &tt));
+        const u32 l = L->size_ql, P = k->size_p;
+        ModDownArgs A{k->plan, k->plan, 0, k->size_q, l, P, L->down->args, L->d_pinv,
+                      tt ? tt : nullptr, tt ? tt + P : nullptr};
+        return mod_down_run2(A, c0, poly, out0, out1, (u64)l * N, batch, s);
+    }
     KsFork fk;  // after dg, ct: joins before they are freed
     RCCHK(fk.open(k, s));
     RCCHK(ks_mod_down_impl(k, L, c0, out0, t, batch, fk.f[0]));

@@ -555,7 +555,7 @@ int plan_ntt_range(ofhe_plan_t p, bool inverse, u32 t0, u32 count, const u64* sr
 }
 
 int plan_ntt_fwd_sub(ofhe_plan_t p, u32 t0, u32 count, u64* y, u64 ystride, const u64* x, u64 xstride, u64* out,
-                     u64 ostride, const u64* scal, u32 batch, hipStream_t s) {
+                     u64 ostride, const u64* scal, u32 batch, hipStream_t s, int parts) {
     if (!p || !p->ctx) return fail(OFHE_ERR_STATE, "plan is NULL or destroyed");
     if (p->log_n < 12) return fail(OFHE_ERR_ARG, "fused forward + subtract needs log_n >= 12");
     if (count == 0 || batch == 0) return OFHE_OK;
@@ -563,7 +563,8 @@ int plan_ntt_fwd_sub(ofhe_plan_t p, u32 t0, u32 count, u64* y, u64 ystride, cons
     HIPCHK(hipSetDevice(p->ctx->device));
     PlanArgs a = args_of(p, t0, count);
     a.sstride = a.dstride = ystride;
-    if (p->log_n > 12) launch_colpass(a, p->spq, p->split8, false, y, y, batch, s);
+    if (p->log_n > 12 && (parts & 1)) launch_colpass(a, p->spq, p->split8, false, y, y, batch, s);
+    if (!(parts & 2)) return post_launch();
     PlanArgs ab = a;
     ab.sstride = ystride;
     ab.dstride = ostride;
