@@ -225,6 +225,32 @@ def test_keyswitch_steps(hip, log_n, sq, sp, dnum, generic):
             assert np.array_equal(host(o), K.ks_mod_down(kp, r0, t)), f"mod down level {l} t {t}"
 
 
+@pytest.mark.parametrize("log_n,sq,sp,dnum,generic", KS_CASES)
+def test_keyswitch_core_levels_and_t(hip, log_n, sq, sp, dnum, generic):
+    """KeySwitchCore bit-exact against the oracle at full and lower levels, for
+    t = 0 (CKKS / BFV) and t = 65537 (BGV), with an odd batch: covers the
+    core's own-tower reads from c (beta <= 4), the merged ModUp launches at
+    full level and the two ModDowns run as one 2 x batch launch set."""
+    H, ctx = hip
+    import torch
+
+    n, q, rq, p, rp, kp, ks = _ks_case(H, ctx, log_n, sq, sp, dnum, generic)
+    rng = np.random.default_rng(300 + log_n)
+    B = 3 if log_n < 16 else 1
+    kb = _uniform(rng, dnum, q + p, n)
+    ka = _uniform(rng, dnum, q + p, n)
+    dkb, dka = dev(kb), dev(ka)
+    for l in sorted({sq, max(1, sq - 1), max(1, kp.alpha - 1)}, reverse=True):
+        c = K.set_format(_uniform(rng, B, q[:l], n), q[:l], rq[:l], True)
+        dc = dev(c)
+        for t in (0, 65537):
+            o0 = torch.empty((B, l, n), dtype=torch.int64, device="cuda")
+            o1 = torch.empty_like(o0)
+            ks.core(l, dc.data_ptr(), dkb.data_ptr(), dka.data_ptr(), o0.data_ptr(), o1.data_ptr(), t, B, stream())
+            r0, r1 = K.ks_core(kp, c, kb, ka, t)
+            assert np.array_equal(host(o0), r0) and np.array_equal(host(o1), r1), f"level {l} t {t}"
+
+
 @pytest.mark.parametrize("log_n,sq,sp,dnum,generic", KS_CASES[:3])
 def test_keyswitch_core_semantics(hip, log_n, sq, sp, dnum, generic):
     """KeySwitchCore on the GPU with real keys: equals the oracle bit for bit
