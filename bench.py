@@ -130,6 +130,8 @@ def parse_args(argv=None):
     ap.add_argument("--ks-steps", type=int, default=10, help="keyswitch sample steps in the default run")
     ap.add_argument("--pcie-batch", type=int, default=32, help="polynomials per chunk of the PCIe-inclusive run")
     ap.add_argument("--pcie-chunks", type=int, default=16, help="chunks of the PCIe-inclusive run (0 = skip)")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="nccl (RCCL, one GPU per rank); gloo = rehearsal of the N-rank path on one GPU")
     ap.add_argument("--launch-check", action="store_true",
                     help="start the ranks and report them (gloo, no GPU): checks the --gpus launcher")
     return ap.parse_args(argv)
@@ -193,16 +195,25 @@ def main():
 # ---------------------------------------------------------------------------
 # Headline: configs[2]
 # ---------------------------------------------------------------------------
-def _dist_setup():
+def _dist_setup(backend="nccl"):
+    """One process per GPU: RCCL ("nccl") over the ranks' own devices.
+    backend "gloo" is a rehearsal mode for a one-GPU box (every rank on
+    cuda:0, host-staged collectives; the C-ABI communicator then fails to come
+    up on a shared device and the ranks fall back together)."""
     import torch
     import torch.distributed as dist
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if backend == "gloo":
+        local = 0
     if world > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "gloo":
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
     return world, rank, local, dev
@@ -258,7 +269,7 @@ def bench_pipeline(args):
     import torch
     import torch.distributed as dist
 
-    world, rank, local, dev = _dist_setup()
+    world, rank, local, dev = _dist_setup(args.dist_backend)
 
     import ofhe_hip as H
     import shard
@@ -600,7 +611,7 @@ def bench_keyswitch_main(args):
     import torch
     import torch.distributed as dist
 
-    world, rank, local, dev = _dist_setup()
+    world, rank, local, dev = _dist_setup(args.dist_backend)
     import ofhe_hip as H
 
     ctx = H.Context(local)

@@ -33,10 +33,22 @@ def evalkey_words(towers: int, log_n: int, dnum: int = 3) -> int:
     return 2 * dnum * (towers + p) << log_n
 
 
+def _host_staged() -> bool:
+    """gloo moves host tensors: device tensors are staged through the host."""
+    import torch.distributed as dist
+
+    return dist.get_backend() == "gloo"
+
+
 def broadcast_evalkey(key, src: int = 0, group=None):
     """Broadcast an evaluation key tensor from `src` to every rank (in place)."""
     import torch.distributed as dist
 
+    if key.is_cuda and _host_staged():
+        h = key.cpu()
+        dist.broadcast(h, src=src, group=group)
+        key.copy_(h)
+        return key
     dist.broadcast(key, src=src, group=group)
     return key
 
@@ -69,6 +81,8 @@ def same_on_all_ranks(t) -> bool:
     import torch.distributed as dist
 
     h = torch.stack([t.sum(), (t * 3).bitwise_xor(t >> 7).sum()]).to(torch.int64)
+    if h.is_cuda and _host_staged():
+        h = h.cpu()
     lo, hi = h.clone(), h.clone()
     dist.all_reduce(lo, op=dist.ReduceOp.MIN)
     dist.all_reduce(hi, op=dist.ReduceOp.MAX)
@@ -112,6 +126,6 @@ def max_over_ranks(value: float, device=None) -> float:
     import torch
     import torch.distributed as dist
 
-    t = torch.tensor([value], dtype=torch.float64, device=device)
+    t = torch.tensor([value], dtype=torch.float64, device=None if _host_staged() else device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
