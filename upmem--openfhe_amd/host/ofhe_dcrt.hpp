@@ -26,6 +26,7 @@
 // std::vector<PolyImpl> (dcrtpoly.h:421), so one launch covers every tower.
 #pragma once
 
+#include <algorithm>
 #include <cstdint>
 #include <cstring>
 #include <map>
@@ -228,9 +229,12 @@ public:
         for (size_t t = 0; t < towers.size(); t++) std::memcpy(towers[t], host_ + t * n, n * sizeof(uint64_t));
     }
     // pinned memory: DMA straight from / to the staging buffer
-    void upload() { check(ofhe_hip_copy_to_device(m_->ctx(), dev(), host_, n_ * 8, nullptr), "Staging::upload"); }
-    void download() {
-        check(ofhe_hip_copy_to_host(m_->ctx(), host_, dev(), n_ * 8, nullptr), "Staging::download");
+    // the first `words` words (default: all) each way
+    void upload(size_t words = SIZE_MAX) {
+        check(ofhe_hip_copy_to_device(m_->ctx(), dev(), host_, std::min(words, n_) * 8, nullptr), "Staging::upload");
+    }
+    void download(size_t words = SIZE_MAX) {
+        check(ofhe_hip_copy_to_host(m_->ctx(), host_, dev(), std::min(words, n_) * 8, nullptr), "Staging::download");
         m_->sync();
     }
 

@@ -23,6 +23,9 @@
 #pragma once
 
 #include <cstdint>
+#include <map>
+#include <memory>
+#include <utility>
 #include <vector>
 
 #include "ofhe_dcrt.hpp"
@@ -61,21 +64,35 @@ inline std::vector<const uint64_t*> cptr(const std::vector<uint64_t*>& p) {
     return std::vector<const uint64_t*>(p.begin(), p.end());
 }
 
+// Pinned staging reused across hook calls: a hook runs once per DCRTPoly
+// operation, and page-locking host memory costs far more than the transfer.
+// One pool per (thread, device), slots grow to the largest size asked for;
+// every hook ends with a synchronous download, so a slot is idle when reused.
+inline Staging& staging(int device, size_t words, int slot = 0) {
+    thread_local std::map<std::pair<int, int>, std::unique_ptr<Staging>> pool;
+    auto& s = pool[{device, slot}];
+    if (!s || s->words() < words) {
+        s.reset();  // release the smaller buffer first
+        s.reset(new Staging(HipManager::getHip(device), words));
+    }
+    return *s;
+}
+
 // DCRTPolyImpl::SwitchFormat (dcrtpoly-impl.h:2518-2524): to_eval = true is
 // COEFFICIENT -> EVALUATION (ForwardTransformToBitReverseInPlace per tower),
 // false the inverse.  The caller flips m_format as the reference does.
 template <class Towers>
 void SwitchFormat(Towers& towers, bool to_eval, int device = 0) {
     TowerView v = view(towers);
-    HipManager* m = HipManager::getHip(device);
     auto plan = PlanCache::get(device, v.log_n, v.q, v.psi);
-    Staging st(m, v.q.size() * (size_t)v.n);
+    const size_t words = v.q.size() * (size_t)v.n;
+    Staging& st = staging(device, words);
     st.gather(cptr(v.data), v.n);
-    st.upload();
+    st.upload(words);
     check(to_eval ? ofhe_hip_ntt_fwd(plan->get(), st.dev(), 1, nullptr)
                   : ofhe_hip_ntt_inv(plan->get(), st.dev(), 1, nullptr),
           "hooks::SwitchFormat");
-    st.download();
+    st.download(words);
     st.scatter(v.data, v.n);
 }
 
@@ -86,19 +103,19 @@ void binary_eq(Towers& a, const Towers& b, int op, const char* what, int device)
     TowerView va = view(a);
     TowerView vb = view(const_cast<Towers&>(b));
     if (va.q != vb.q || va.n != vb.n) throw math_error(std::string(what) + ": Modulus missmatch");
-    HipManager* m = HipManager::getHip(device);
     auto plan = PlanCache::get(device, va.log_n, va.q, va.psi);
     const size_t words = va.q.size() * (size_t)va.n;
-    Staging sa(m, words), sb(m, words);
+    Staging& sa = staging(device, words, 0);
+    Staging& sb = staging(device, words, 1);
     sa.gather(cptr(va.data), va.n);
     sb.gather(cptr(vb.data), vb.n);
-    sa.upload();
-    sb.upload();
+    sa.upload(words);
+    sb.upload(words);
     int rc = op == 0   ? ofhe_hip_modmul_vv(plan->get(), sa.dev(), sb.dev(), sa.dev(), 1, nullptr)
              : op == 1 ? ofhe_hip_modadd_vv(plan->get(), sa.dev(), sb.dev(), sa.dev(), 1, nullptr)
                        : ofhe_hip_modsub_vv(plan->get(), sa.dev(), sb.dev(), sa.dev(), 1, nullptr);
     check(rc, what);
-    sa.download();
+    sa.download(words);
     sa.scatter(va.data, va.n);
 }
 }  // namespace detail
@@ -133,7 +150,7 @@ void ApproxSwitchCRTBasis(const TowersQ& x, TowersP& out, const std::vector<uint
     if (QHatInvModq.size() != vx.q.size() || QHatModp.size() != vx.q.size() * vo.q.size())
         throw math_error("hooks::ApproxSwitchCRTBasis: table sizes");
     HipManager* m = HipManager::getHip(device);
-    static std::mutex mu;
+    static std::mutex mu;  // the converter cache is process-wide
     static std::map<std::vector<uint64_t>, std::shared_ptr<ofhe_bconv_s>> cache;
     std::shared_ptr<ofhe_bconv_s> bc;
     {
@@ -153,11 +170,13 @@ void ApproxSwitchCRTBasis(const TowersQ& x, TowersP& out, const std::vector<uint
         }
         bc = e;
     }
-    Staging sx(m, vx.q.size() * (size_t)vx.n), so(m, vo.q.size() * (size_t)vo.n);
+    const size_t wx = vx.q.size() * (size_t)vx.n, wo = vo.q.size() * (size_t)vo.n;
+    Staging& sx = staging(device, wx, 0);
+    Staging& so = staging(device, wo, 1);
     sx.gather(cptr(vx.data), vx.n);
-    sx.upload();
+    sx.upload(wx);
     check(ofhe_hip_approx_switch_crt_basis(bc.get(), sx.dev(), so.dev(), 1, nullptr), "hooks::ApproxSwitchCRTBasis");
-    so.download();
+    so.download(wo);
     so.scatter(vo.data, vo.n);
 }
 
