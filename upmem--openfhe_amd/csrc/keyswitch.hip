@@ -35,6 +35,11 @@ using namespace ofhe;
 #ifndef OFHE_KS_MD2
 #define OFHE_KS_MD2 1
 #endif
+// side streams the ModUp digits are spread over (digit j on stream j mod n)
+#ifndef OFHE_KS_NSIDE
+#define OFHE_KS_NSIDE 2
+#endif
+constexpr int KS_NSIDE = OFHE_KS_NSIDE;
 
 namespace {
 
@@ -266,7 +271,7 @@ struct ofhe_ks_s {
     u32 log_n = 0, size_q = 0, size_p = 0, num_part_q = 0, alpha = 0;
     std::vector<u64> q, p;
     ofhe_plan_t plan = nullptr;  // towers q[0..size_q) then p[0..size_p)
-    hipStream_t side[2] = {nullptr, nullptr};  // fork streams (OFHE_KS_STREAMS=1: none)
+    hipStream_t side[KS_NSIDE] = {};  // fork streams (OFHE_KS_STREAMS=1: none)
     std::mutex mu;
     std::map<u32, KsLevel*> levels;
 };
@@ -317,7 +322,8 @@ int ofhe_hip_ks_create(ofhe_ctx_t ctx, uint32_t log_n, uint32_t size_q, const ui
     const char* ns = getenv("OFHE_KS_STREAMS");
     if (!(ns && atoi(ns) == 1)) {
         hipError_t e = hipSetDevice(ctx->device);
-        for (int i = 0; i < 2 && e == hipSuccess; i++) e = hipStreamCreateWithFlags(&k->side[i], hipStreamNonBlocking);
+        for (int i = 0; i < KS_NSIDE && e == hipSuccess; i++)
+            e = hipStreamCreateWithFlags(&k->side[i], hipStreamNonBlocking);
         if (e != hipSuccess) {
             for (auto& st : k->side)
                 if (st) (void)hipStreamDestroy(st);
@@ -464,24 +470,24 @@ static int level_t_tables(ofhe_ks_t k, KsLevel* L, u64 t, const TowerScalar** ou
 // any stream-ordered Scratch its work uses, so it joins before they are freed.
 struct KsFork {
     hipStream_t parent = nullptr;
-    hipStream_t f[2] = {nullptr, nullptr};
-    hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
+    hipStream_t f[KS_NSIDE] = {};
+    hipEvent_t ev[KS_NSIDE + 1] = {};
     bool forked = false;
     int open(ofhe_ks_t k, hipStream_t s) {
-        parent = f[0] = f[1] = s;
+        parent = s;
+        for (auto& x : f) x = s;
         if (!k->side[0]) return OFHE_OK;
         for (auto& e : ev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
         HIPCHK(hipEventRecord(ev[0], s));
-        for (int i = 0; i < 2; i++) HIPCHK(hipStreamWaitEvent(k->side[i], ev[0], 0));
-        f[0] = k->side[0];
-        f[1] = k->side[1];
+        for (int i = 0; i < KS_NSIDE; i++) HIPCHK(hipStreamWaitEvent(k->side[i], ev[0], 0));
+        for (int i = 0; i < KS_NSIDE; i++) f[i] = k->side[i];
         forked = true;
         return OFHE_OK;
     }
     int join() {
         if (!forked) return OFHE_OK;
         forked = false;
-        for (int i = 0; i < 2; i++) {
+        for (int i = 0; i < KS_NSIDE; i++) {
             HIPCHK(hipEventRecord(ev[1 + i], f[i]));
             HIPCHK(hipStreamWaitEvent(parent, ev[1 + i], 0));
         }
@@ -511,7 +517,7 @@ static int ks_precompute_impl(ofhe_ks_t k, KsLevel* L, uint32_t size_ql, const u
     const u64 N = 1ull << k->log_n, l = size_ql, P = k->size_p, poly = (l + P) * N, ds = L->beta * poly;
     for (u32 j = 0; j < L->beta; j++) {
         const u32 st = L->start[j], n = L->cnt[j];
-        hipStream_t s = fk.f[j & 1];  // digits are independent
+        hipStream_t s = fk.f[j % KS_NSIDE];  // digits are independent
         u64* slot = digits + j * poly;
         // partsCt[j] in coefficient form (keyswitch-hybrid.cpp:384-385)
         RCCHK(plan_ntt_range(k->plan, true, st, n, c + st * N, slot + st * N, l * N, ds, batch, s));
