@@ -51,10 +51,13 @@ enum {
 typedef struct ofhe_ctx_s* ofhe_ctx_t;   /* one per device (PimManager::getPim) */
 typedef struct ofhe_plan_s* ofhe_plan_t; /* NTT plan: (N, towers, q[], psi[])  */
 
-/* Thread-local description of the last failure in this thread. */
+/* Thread-local description of the last failure in this thread: the message
+ * OPENFHE_THROW(math_error, msg) carries (src/core/include/utils/exception.h:162);
+ * the fork's PIM layer instead aborts in DPU_ASSERT (PimManager.cpp:5-37). */
 const char* ofhe_hip_last_error(void);
 
-/* Library version string ("ofhe-hip <ver> gfx950"). */
+/* Library version string ("ofhe-hip <ver> gfx950"); no reference counterpart
+ * (the fork's kernel binaries are located by path, pim/kernel.h:4-8). */
 const char* ofhe_hip_version(void);
 
 /* ---- device context: replaces PimManager::getPim(nr_dpus, profile),
@@ -163,8 +166,9 @@ int ofhe_hip_modsub_scalar(ofhe_plan_t plan, const uint64_t* a, const uint64_t* 
 int ofhe_hip_modadd_scalar_at(ofhe_plan_t plan, const uint64_t* a, uint64_t index, const uint64_t* s,
                               uint64_t* c, uint32_t batch, void* stream);
 
-/* Synthetic inputs for benchmarks and tests, no reference
- * counterpart: dst[b][t][i] = splitmix64 draw i + 1 of the stream seeded
+/* Synthetic inputs for benchmarks and tests; no reference
+ * counterpart (the benchmark draws uniform vectors on the host,
+ * poly-benchmark-16k.cpp:45-70): dst[b][t][i] = splitmix64 draw i + 1 of the stream seeded
  * 0x5EED ^ ((batch_offset + b) << 20) ^ (t << 8) ^ seed, mod q[t] -- what the
  * CPU oracle's generator (oracle_fill_uniform) produces for the same seed. */
 int ofhe_hip_fill_uniform(ofhe_plan_t plan, uint64_t* dst, uint32_t batch, uint32_t batch_offset, uint64_t seed,
@@ -177,7 +181,8 @@ int ofhe_hip_fill_uniform(ofhe_plan_t plan, uint64_t* dst, uint32_t batch, uint3
 int ofhe_hip_ntt_mul_intt(ofhe_plan_t plan, const uint64_t* a, const uint64_t* b, uint64_t* c,
                           uint32_t batch, void* stream);
 
-/* One launch of the pipeline above, for per-kernel timing (bench.py):
+/* One launch of the pipeline above, for per-kernel timing (bench.py); no
+ * reference counterpart (the reference's loop is per tower, dcrtpoly-impl.h:2518-2524):
  * stage 0 = forward column pass (a -> c), 1 = block pass (forward tail,
  * Hadamard with b, inverse head; reads c, or a when log_n <= 12),
  * 2 = inverse column pass (c -> c).  Stages 0 and 2 are no-ops for

@@ -86,3 +86,25 @@ def test_argument_errors_without_device():
     assert L.ofhe_hip_last_error()  # a message is set
     with pytest.raises(H.MathError):
         H._check(L.ofhe_hip_ntt_inv(null, null, 1, null))
+
+
+def test_every_entry_point_cites_the_reference():
+    """Each declaration's comment block cites the reference file:line it replaces,
+    or says it has no reference counterpart (the drop-in contract)."""
+    import re
+
+    lines = open(HEADER).read().split("\n")
+    comment, missing = [], []
+    for line in lines:
+        t = line.strip()
+        if t.startswith(("/*", "*", "//")) or t.endswith("*/"):
+            comment.append(t)
+            continue
+        m = re.search(r"\b(ofhe_hip_\w+)\s*\(", line)
+        if m:
+            c = " ".join(comment)
+            if not (re.search(r"\.(h|cpp|c):\d+", c) or "no reference counterpart" in c):
+                missing.append(m.group(1))
+        if not t:
+            comment = []
+    assert not missing, missing
