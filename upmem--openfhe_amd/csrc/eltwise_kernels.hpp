@@ -16,30 +16,55 @@ enum { ELT_MUL = 0, ELT_ADD = 1, ELT_SUB = 2, ELT_MULS = 3, ELT_ADDS = 4, ELT_SU
 __device__ __forceinline__ u64 modadd_fast(u64 a, u64 b, u64 q) { return csub(a + b, q); }
 __device__ __forceinline__ u64 modsub_fast(u64 a, u64 b, u64 q) { return a < b ? a + q - b : a - b; }
 
-// a, b, c: [batch][towers][N], vector (.) vector.
+// a, b, c: [batch][towers][N], vector (.) vector.  Each thread moves
+// elt_unroll(OP) independent 16-byte pairs, all loads issued before any
+// arithmetic, streaming hints on data.  The host launches one thread per
+// elt_unroll(OP) pairs (no grid-stride at the sizes used): measured at N=2^16,
+// 16 towers, batch 256 on MI355X, a 4096-block grid-stride launch moved
+// 4.5-4.7 TB/s, the full grid 6.0-6.3 TB/s (ModMul best with 2 pairs per
+// thread, the add/sub/scalar ops with 1; DESIGN.md "Element-wise bandwidth").
+#ifdef OFHE_ELT_UNROLL
+__host__ __device__ constexpr int elt_unroll(int) { return OFHE_ELT_UNROLL; }
+#else
+__host__ __device__ constexpr int elt_unroll(int op) { return op == ELT_MUL ? 2 : 1; }
+#endif
 template <int OP>
 __global__ __launch_bounds__(256) void k_eltwise(const TowerConst* __restrict__ tcs,
                                                  const u64* a, const u64* b, u64* c, u64 npairs,
                                                  u32 log_n, u32 towers) {
+    constexpr int ELT_U = elt_unroll(OP);
     const u64 stride = (u64)gridDim.x * blockDim.x;
-    for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < npairs; i += stride) {
-        const u64 e = 2 * i;
-        const u32 t = (u32)((e >> log_n) % towers);
-        const TowerConst tc = tcs[t];
-        const ulonglong2 x = reinterpret_cast<const ulonglong2*>(a)[i];
-        const ulonglong2 y = reinterpret_cast<const ulonglong2*>(b)[i];
-        ulonglong2 r;
-        if (OP == ELT_MUL) {
-            r.x = barrett_ref(x.x, y.x, tc.q, tc.mu, tc.nshift);
-            r.y = barrett_ref(x.y, y.y, tc.q, tc.mu, tc.nshift);
-        } else if (OP == ELT_ADD) {
-            r.x = modadd_fast(x.x, y.x, tc.q);
-            r.y = modadd_fast(x.y, y.y, tc.q);
-        } else {
-            r.x = modsub_fast(x.x, y.x, tc.q);
-            r.y = modsub_fast(x.y, y.y, tc.q);
+    for (u64 i0 = (u64)blockIdx.x * blockDim.x + threadIdx.x; i0 < npairs; i0 += stride * ELT_U) {
+        u64x2 x[ELT_U], y[ELT_U];
+#pragma unroll
+        for (int u = 0; u < ELT_U; u++) {
+            const u64 i = i0 + u * stride;
+            if (i < npairs) {
+                x[u] = ld2_s(a + 2 * i);
+                y[u] = ld2_s(b + 2 * i);
+            }
         }
-        reinterpret_cast<ulonglong2*>(c)[i] = r;
+#pragma unroll
+        for (int u = 0; u < ELT_U; u++) {
+            const u64 i = i0 + u * stride;
+            if (i >= npairs) break;
+            const u32 t = (u32)((2 * i) >> log_n) % towers;  // row < 2^32: 32-bit modulo
+            u64x2 r;
+            if (OP == ELT_MUL) {
+                const TowerConst tc = tcs[t];
+                r.x = barrett_ref(x[u].x, y[u].x, tc.q, tc.mu, tc.nshift);
+                r.y = barrett_ref(x[u].y, y[u].y, tc.q, tc.mu, tc.nshift);
+            } else if (OP == ELT_ADD) {
+                const u64 q = tcs[t].q;
+                r.x = modadd_fast(x[u].x, y[u].x, q);
+                r.y = modadd_fast(x[u].y, y[u].y, q);
+            } else {
+                const u64 q = tcs[t].q;
+                r.x = modsub_fast(x[u].x, y[u].x, q);
+                r.y = modsub_fast(x[u].y, y[u].y, q);
+            }
+            st2_s(c + 2 * i, r);
+        }
     }
 }
 
@@ -59,27 +84,38 @@ __global__ __launch_bounds__(256) void k_scalar(ScalarPack S, const u64* a, u64*
                                                 u32 cnt, u32 t0, u32 towers) {
     const u64 stride = (u64)gridDim.x * blockDim.x;
     const u64 mask = (1ull << log_n) - 1;
-    for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < npairs; i += stride) {
-        const u64 e = 2 * i;
-        const u64 row = e >> log_n;  // b * cnt + tl
-        const u32 tl = (u32)(row % cnt);
-        const u64 b = row / cnt;
-        const u64 at = ((b * towers + t0 + tl) << log_n) | (e & mask);
-        const u64 q = S.v[3 * tl], s = S.v[3 * tl + 1];
-        const ulonglong2 x = *reinterpret_cast<const ulonglong2*>(a + at);
-        ulonglong2 r;
-        if (OP == ELT_MULS) {
-            const u64 sp = S.v[3 * tl + 2];
-            r.x = shoup_canon(x.x, s, sp, q);
-            r.y = shoup_canon(x.y, s, sp, q);
-        } else if (OP == ELT_ADDS) {
-            r.x = modadd_fast(x.x, s, q);
-            r.y = modadd_fast(x.y, s, q);
-        } else {
-            r.x = modsub_fast(x.x, s, q);
-            r.y = modsub_fast(x.y, s, q);
+    constexpr int ELT_U = elt_unroll(OP);
+    for (u64 i0 = (u64)blockIdx.x * blockDim.x + threadIdx.x; i0 < npairs; i0 += stride * ELT_U) {
+        u64x2 x[ELT_U];
+        u64 at[ELT_U];
+#pragma unroll
+        for (int u = 0; u < ELT_U; u++) {
+            const u64 i = i0 + u * stride;
+            const u64 e = 2 * i;
+            const u32 row = (u32)(e >> log_n);  // b * cnt + tl (< 2^32: batch * towers fits a launch)
+            at[u] = (((u64)(row / cnt) * towers + t0 + row % cnt) << log_n) | (e & mask);
+            if (i < npairs) x[u] = ld2_s(a + at[u]);
         }
-        *reinterpret_cast<ulonglong2*>(c + at) = r;
+#pragma unroll
+        for (int u = 0; u < ELT_U; u++) {
+            const u64 i = i0 + u * stride;
+            if (i >= npairs) break;
+            const u32 tl = (u32)((2 * i) >> log_n) % cnt;
+            const u64 q = S.v[3 * tl], s = S.v[3 * tl + 1];
+            u64x2 r;
+            if (OP == ELT_MULS) {
+                const u64 sp = S.v[3 * tl + 2];
+                r.x = shoup_canon(x[u].x, s, sp, q);
+                r.y = shoup_canon(x[u].y, s, sp, q);
+            } else if (OP == ELT_ADDS) {
+                r.x = modadd_fast(x[u].x, s, q);
+                r.y = modadd_fast(x[u].y, s, q);
+            } else {
+                r.x = modsub_fast(x[u].x, s, q);
+                r.y = modsub_fast(x[u].y, s, q);
+            }
+            st2_s(c + at[u], r);
+        }
     }
 }
 
@@ -106,9 +142,9 @@ static __global__ __launch_bounds__(256) void k_fill_uniform(const TowerConst* _
                                                       u32 log_n, u32 towers, u32 b0, u64 seed) {
     const u64 stride = (u64)gridDim.x * blockDim.x;
     for (u64 e = (u64)blockIdx.x * blockDim.x + threadIdx.x; e < words; e += stride) {
-        const u64 row = e >> log_n;
-        const u32 t = (u32)(row % towers);
-        const u64 b = row / towers + b0;
+        const u32 row = (u32)(e >> log_n);
+        const u32 t = row % towers;
+        const u64 b = (u64)(row / towers) + b0;
         const u64 i = e & ((1ull << log_n) - 1);
         u64 z = (0x5EEDull ^ (b << 20) ^ ((u64)t << 8) ^ seed) + (i + 1) * 0x9E3779B97F4A7C15ull;
         z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;

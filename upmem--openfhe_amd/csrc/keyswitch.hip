@@ -51,9 +51,12 @@ u64 prod_mod(const u64* ms, u32 n, u32 skip, u64 m) {
     return r;
 }
 
+// one thread per item for the streaming kernels (grid-stride only past 2^30
+// threads): a full grid keeps more bytes in flight than a capped grid-stride
+// launch (ofhe_hip.hip eltwise, DESIGN.md "Element-wise bandwidth")
 u32 grid_for(u64 items) {
     u64 b = (items + 255) / 256;
-    if (b > 256 * 16) b = 256 * 16;
+    if (b > (1u << 22)) b = 1u << 22;
     return (u32)(b ? b : 1);
 }
 

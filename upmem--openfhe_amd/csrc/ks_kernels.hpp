@@ -23,8 +23,8 @@ struct PairIndex {
 };
 __device__ __forceinline__ PairIndex pair_index(u64 i, u32 log_n, u32 towers) {
     const u64 e = 2 * i;
-    const u64 row = e >> log_n;
-    return PairIndex{(u32)(row / towers), (u32)(row % towers), (u32)(e & ((1ull << log_n) - 1))};
+    const u32 row = (u32)(e >> log_n);  // batch * towers < 2^32 for any buffer that fits in HBM: 32-bit divide
+    return PairIndex{row / towers, row % towers, (u32)(e & ((1ull << log_n) - 1))};
 }
 
 // out = x * s_t mod q_t (NativeVectorT::ModMulEq(scalar), mubintvecnat.cpp:310-332)
@@ -267,7 +267,7 @@ __global__ __launch_bounds__(256) void k_automorphism(const TowerConst* __restri
             const u32 irev = __builtin_bitreverse32((u32)((jk >> 1) & mask)) >> (32 - log_n);
             dst[base + jrev] = src[base + irev];
         } else {
-            const u64 q = tcs[row % towers].q;
+            const u64 q = tcs[(u32)row % towers].q;
             const u64 jk = ((u64)k * j) & m2;
             const u64 v = src[base + j];
             dst[base + (jk & mask)] = ((jk >> log_n) & 1) ? q - v : v;

@@ -674,6 +674,11 @@ int ofhe_hip_ntt_mul_intt_stage(ofhe_plan_t p, int stage, const uint64_t* a_, co
     return post_launch();
 }
 
+// grid cap of the streaming element-wise launches (grid-stride beyond it;
+// 2^22 blocks = 2^31 pairs per pass, never reached by a launch of the sizes used)
+#ifndef OFHE_ELT_GRID
+#define OFHE_ELT_GRID (1u << 22)
+#endif
 template <int OP>
 static int eltwise(ofhe_plan_t p, const u64* a, const u64* b, u64* c, u32 batch, void* stream) {
     int rc = check_common(p, batch);
@@ -681,8 +686,8 @@ static int eltwise(ofhe_plan_t p, const u64* a, const u64* b, u64* c, u32 batch,
     if (!a || !b || !c) return fail(OFHE_ERR_ARG, "NULL data pointer");
     HIPCHK(hipSetDevice(p->ctx->device));
     const u64 npairs = (u64)batch * p->towers * ((u64)1 << p->log_n) / 2;
-    u64 blocks = (npairs + 255) / 256;
-    if (blocks > 256 * 16) blocks = 256 * 16;
+    u64 blocks = (npairs + 256 * elt_unroll(OP) - 1) / (256 * elt_unroll(OP));
+    if (blocks > OFHE_ELT_GRID) blocks = OFHE_ELT_GRID;
     hipLaunchKernelGGL((k_eltwise<OP>), dim3((u32)blocks), dim3(256), 0, pick(stream), p->d_tc, a, b,
                        c, npairs, p->log_n, p->towers);
     return post_launch();
@@ -730,8 +735,8 @@ static int scalar_op(ofhe_plan_t p, const u64* a, const u64* s, u64* c, u32 batc
                                p->log_n, cnt, t0, p->towers, idx);
         } else {
             const u64 npairs = ((u64)batch * cnt << p->log_n) / 2;
-            u64 blocks = (npairs + 255) / 256;
-            if (blocks > 256 * 16) blocks = 256 * 16;
+            u64 blocks = (npairs + 256 * elt_unroll(OP) - 1) / (256 * elt_unroll(OP));
+            if (blocks > OFHE_ELT_GRID) blocks = OFHE_ELT_GRID;
             hipLaunchKernelGGL((k_scalar<OP>), dim3((u32)blocks), dim3(256), 0, st, S, a, c, npairs, p->log_n, cnt,
                                t0, p->towers);
         }
@@ -765,7 +770,7 @@ int ofhe_hip_fill_uniform(ofhe_plan_t p, uint64_t* dst, uint32_t batch, uint32_t
     HIPCHK(hipSetDevice(p->ctx->device));
     const u64 words = (u64)batch * p->towers << p->log_n;
     u64 blocks = (words + 255) / 256;
-    if (blocks > 256 * 64) blocks = 256 * 64;
+    if (blocks > (1u << 22)) blocks = 1u << 22;
     hipLaunchKernelGGL(k_fill_uniform, dim3((u32)blocks), dim3(256), 0, pick(stream), p->d_tc, dst, words,
                        p->log_n, p->towers, batch_offset, seed);
     return post_launch();
