@@ -126,22 +126,27 @@ def test_approx_mod_down(hip, log_n, sq, sp, generic, t):
     assert np.array_equal(host(out), K.approx_mod_down(x, q, rq, p, rp, t))
 
 
-@pytest.mark.parametrize("sq", [1, 7, 16])
-def test_base_conversion_max_sums(hip, sq):
-    """Largest sums the limb kernel reduces: every input q_i - 1 (q_i up to
-    2^60 - 1), QHatInvModq = 1 and every QHatModp entry p_j - 1, for output
-    moduli from 2 to 2^60 - 1 (powers of two included).  Expected values by
-    Python integers: out_j = sum_i (q_i - 1)(p_j - 1) mod p_j."""
+@pytest.mark.parametrize("sq,reps", [(1, 1), (7, 1), (16, 1), (17, 1), (32, 1), (33, 1), (16, 8)])
+def test_base_conversion_max_sums(hip, sq, reps):
+    """Extreme sums for every base-conversion kernel: inputs q_i - 1 (q_i up
+    to 2^60 - 1) and 0x007F7F7F7F7F7F80 (seven signed base-256 digits of
+    -128 in the matrix-core kernel's digit split), QHatInvModq = 1 and every
+    QHatModp entry p_j - 1, for output moduli from 2 to 2^60 - 1 (powers of
+    two included).  size_q <= 32 with a small target set runs k_bconv_mma
+    (K-steps 1, 2, 4, 5, 8), size_q = 33 the 128-bit k_bconv, and 16 sources
+    into 72 targets (fragment table above the LDS budget) k_bconv_limb.
+    Expected values by Python integers: out_j = sum_i x_i (p_j - 1) mod p_j."""
     H, ctx = hip
     import torch
 
     log_n, n = 5, 32
     q = [(1 << 60) - 1 - 2 * i for i in range(sq)]
-    p = [2, 3, 1 << 31, (1 << 32) + 15, (1 << 45) + 7, (1 << 59) + 1, (1 << 60) - 1, 1 << 59, 97]
+    p = [2, 3, 1 << 31, (1 << 32) + 15, (1 << 45) + 7, (1 << 59) + 1, (1 << 60) - 1, 1 << 59, 97] * reps
     bc = H.BaseConverter(ctx, log_n, q, p, [1] * sq, [pj - 1 for _ in q for pj in p])
     rng = np.random.default_rng(sq)
     x = np.stack([np.full(n, qi - 1, np.uint64) for qi in q])
     x[:, 1::2] = np.stack([rng.integers(0, qi, size=n // 2, dtype=np.uint64) for qi in q])
+    x[:, 2::4] = np.uint64(0x007F7F7F7F7F7F80)
     dx = dev(x[None])
     out = torch.zeros((1, len(p), n), dtype=torch.int64, device="cuda")
     bc.switch(dx.data_ptr(), out.data_ptr(), 1, stream())

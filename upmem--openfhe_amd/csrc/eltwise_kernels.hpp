@@ -174,6 +174,9 @@ struct BconvArgs {
     u64 out_stride;       // words between batch entries of out (sizeP * N when dense)
     u32 log_n, size_q, size_p;
     u32 gap_at, gap;      // output tower j >= gap_at is written at j + gap (key-switch digit slot)
+    const void* mm_tab;   // k_bconv_mma fragment table + constants (bconv_mma.hpp), or null
+    u32 mm_tiles, mm_ks;  // its target tiles (4 towers) and K-steps (4 source towers)
+    u32 lazy_out;         // internal callers: outputs in [0, 4p) (a forward NTT follows)
 };
 
 template <int PT>

@@ -13,6 +13,7 @@
 
 #include "../../include/ofhe_hip.h"
 #include "eltwise_kernels.hpp"
+#include "bconv_mma.hpp"
 
 namespace ofhe {
 typedef unsigned __int128 u128;

@@ -131,6 +131,7 @@ int mod_down_run(const ModDownArgs& A, const u64* x, u64 xstride, u64* out, u64 
     B.out_stride = qs;
     B.gap_at = A.size_q;
     B.gap = 0;
+    B.lazy_out = 1;  // a forward NTT (after an optional tower scale) follows
     RCCHK(bconv_run(B, sp.w(), sq.w(), batch, s));
     if (A.t_q) RCCHK(scale_towers(A.t_q, sq.w(), sq.w(), qs, qs, batch, A.size_q, log_n, s));
     // SetFormat(EVALUATION), then ans_i = (x_i - switched_i) * PInvModq_i
@@ -163,6 +164,7 @@ int mod_down_run2(const ModDownArgs& A, const u64* x0, u64 xstride, u64* out0, u
     B.out_stride = qs;
     B.gap_at = A.size_q;
     B.gap = 0;
+    B.lazy_out = 1;  // a forward NTT (after an optional tower scale) follows
     RCCHK(bconv_run(B, sp.w(), sq.w(), b2, s));
     if (A.t_q) RCCHK(scale_towers(A.t_q, sq.w(), sq.w(), qs, qs, b2, A.size_q, log_n, s));
     const u64* x1 = x0 + (u64)batch * xstride;
@@ -195,6 +197,7 @@ int ofhe_hip_approx_mod_up(ofhe_plan_t pq, ofhe_plan_t pp, ofhe_bconv_t bc, int 
     const u64 N = 1ull << pq->log_n, Q = pq->towers, P = pp->towers, qp = (Q + P) * N;
     BconvArgs B = bc->args;
     B.out_stride = qp;
+    B.lazy_out = 1;  // the P towers go through a forward NTT below
     if (eval_form) {
         // coefficient copy of x (SetFormat(COEFFICIENT), 1097-1100) into the Q slots
         RCCHK(plan_ntt_range(pq, true, 0, (u32)Q, x, out, Q * N, qp, batch, s));
@@ -529,6 +532,7 @@ static int ks_precompute_impl(ofhe_ks_t k, KsLevel* L, uint32_t size_ql, const u
         B.in_stride = B.out_stride = ds;
         B.gap_at = st;
         B.gap = n;
+        B.lazy_out = 1;  // every complement tower goes through a forward NTT below
         RCCHK(bconv_run(B, slot + st * N, slot, batch, s));
         // complement towers to evaluation form (394)
         RCCHK(plan_ntt_range(k->plan, false, 0, st, slot, slot, ds, ds, batch, s));

@@ -784,6 +784,56 @@ template <class T>
 T* pred_of(T* qhlimb, u32 qrows, u32 ppad) { return qhlimb + (size_t)qrows * ppad; }
 }  // namespace
 
+// k_bconv_mma's LDS image (bconv_mma.hpp): A-operand fragments
+// [tiles][ks][64 lanes][16 int8], then BmRed[4 tiles], then BmSrc[4 ks].
+// qhinv: [size_q][2] (canonical QHatInvModq, Shoup precon); qhmodp: [size_q][size_p], canonical.
+static bool bconv_mma_table(u32 size_q, u32 size_p, const u64* q, const u64* p, const u64* qhinv,
+                            const u64* qhmodp, std::vector<unsigned char>& tab, u32& tiles, u32& ks) {
+    ks = (size_q + 3) / 4;
+    tiles = (size_p + 3) / 4;
+    const size_t fbytes = (size_t)tiles * ks * 1024;
+    const size_t bytes = fbytes + 4 * (size_t)tiles * sizeof(BmRed) + 4 * (size_t)ks * sizeof(BmSrc);
+    if (size_q > BCONV_MMA_QMAX || bytes > BCONV_MMA_LDS_MAX) {
+        tiles = ks = 0;
+        return false;
+    }
+    tab.assign(bytes, 0);
+    // h_{(i,a),j} = 2^(8a) QHatModp_{i,j} mod p_j, as signed base-256 digits
+    for (u32 t = 0; t < tiles; t++)
+        for (u32 s = 0; s < ks; s++)
+            for (u32 l = 0; l < 64; l++) {
+                const u32 r = l & 31, kh = l >> 5;
+                const u32 dh = (r >> 2) & 1, reg = (r & 3) + 4 * (r >> 3);
+                const u32 j = 4 * t + 2 * dh + (reg >> 3), bd = reg & 7;
+                for (u32 e = 0; e < 16; e++) {
+                    const u32 i = 4 * s + 2 * kh + (e >> 3), a = e & 7;
+                    if (i >= size_q || j >= size_p) continue;
+                    const u64 hv = mulmod(powmod(2, 8 * a, p[j]), qhmodp[(size_t)i * size_p + j], p[j]);
+                    const u64 z = hv + DIGIT_BIAS;
+                    tab[(((size_t)t * ks + s) * 64 + l) * 16 + e] = (unsigned char)(((z >> (8 * bd)) & 0xFF) ^ 0x80);
+                }
+            }
+    BmRed* red = reinterpret_cast<BmRed*>(tab.data() + fbytes);
+    for (u32 j = 0; j < size_p; j++) {
+        BmRed& R = red[j];
+        u64 lr[3];
+        limb_red_consts(p[j], lr);
+        R.p = p[j];
+        R.np = 0 - p[j];
+        R.r60 = lr[0];
+        R.r60p = lr[1];
+        R.mu1 = lr[2];
+        const u128 k = (((u128)1 << 79) + p[j] - 1) / p[j];
+        const u128 bias = k * p[j];
+        R.bhi = (u64)(bias >> 32) - (1ull << 15);
+        R.blo = (u64)(bias & 0xFFFFFFFFull) + (1ull << 47);
+        R.p2 = 2 * p[j];
+    }
+    BmSrc* src = reinterpret_cast<BmSrc*>(red + 4 * tiles);
+    for (u32 i = 0; i < size_q; i++) src[i] = BmSrc{q[i], qhinv[2 * i], qhinv[2 * i + 1], 0};
+    return true;
+}
+
 int ofhe_hip_bconv_create(ofhe_ctx_t ctx, uint32_t log_n, uint32_t size_q, uint32_t size_p,
                           const uint64_t* q, const uint64_t* p, const uint64_t* qhat_inv_modq,
                           const uint64_t* qhat_modp, ofhe_bconv_t* out) {
@@ -825,12 +875,24 @@ int ofhe_hip_bconv_create(ofhe_ctx_t ctx, uint32_t log_n, uint32_t size_q, uint3
         pmu[2 * j + 1] = (u64)(mu >> 64);
         limb_red_consts(p[j], pred_of(qhlimb, qrows, ppad) + 3 * j);
     }
+    // the matrix-core kernel's table (bconv_mma.hpp), appended 16-byte aligned
+    u32 mm_tiles = 0, mm_ks = 0;
+    size_t mm_off = 0;
+    {
+        std::vector<unsigned char> tab;
+        if (bconv_mma_table(size_q, size_p, q, p, qhinv, qhmodp, tab, mm_tiles, mm_ks)) {
+            mm_off = (h.size() + 1) & ~(size_t)1;
+            h.resize(mm_off + tab.size() / 8);
+            std::memcpy(h.data() + mm_off, tab.data(), tab.size());
+        }
+    }
+    const size_t words_all = h.size();
     ofhe_bconv_s* b = new (std::nothrow) ofhe_bconv_s();
     if (!b) return fail(OFHE_ERR_NOMEM, "bconv allocation failed");
     b->ctx = ctx;
     hipError_t e = hipSetDevice(ctx->device);
-    if (e == hipSuccess) e = hipMalloc(&b->d_mem, words * sizeof(u64));
-    if (e == hipSuccess) e = hipMemcpy(b->d_mem, h.data(), words * sizeof(u64), hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMalloc(&b->d_mem, words_all * sizeof(u64));
+    if (e == hipSuccess) e = hipMemcpy(b->d_mem, h.data(), words_all * sizeof(u64), hipMemcpyHostToDevice);
     if (e != hipSuccess) {
         (void)hipFree(b->d_mem);
         delete b;
@@ -851,6 +913,9 @@ int ofhe_hip_bconv_create(ofhe_ctx_t ctx, uint32_t log_n, uint32_t size_q, uint3
     A.out_stride = (u64)size_p << log_n;
     A.gap_at = size_p;
     A.gap = 0;
+    A.mm_tab = mm_tiles ? (const void*)(b->d_mem + mm_off) : nullptr;
+    A.mm_tiles = mm_tiles;
+    A.mm_ks = mm_ks;
     *out = b;
     return OFHE_OK;
 }
@@ -869,7 +934,34 @@ int bconv_run(const BconvArgs& A, const u64* x, u64* out, u32 batch, hipStream_t
     const u64 total = (u64)batch << A.log_n;
     const u64 blocks = (total + 255) / 256;
     if (blocks >= (1ull << 31)) return fail(OFHE_ERR_ARG, "batch too large");
-    static const bool generic = getenv("OFHE_BCONV_GENERIC") != nullptr;  // A/B switch
+    static const bool generic = getenv("OFHE_BCONV_GENERIC") != nullptr;  // A/B switches
+    static const bool limb = getenv("OFHE_BCONV_LIMB") != nullptr;
+    if (OFHE_BCONV_MMA && A.mm_tab && A.log_n >= 5 && !generic && !limb) {
+        const u64 groups = total >> 5;
+        const u32 wpb = BCONV_MMA_THREADS / 64;
+        u64 grid = (groups + wpb - 1) / wpb;
+        const u64 cap = 256ull * BCONV_MMA_BLOCKS_PER_CU;
+        if (grid > cap) grid = cap;
+        const size_t lds = (size_t)A.mm_tiles * A.mm_ks * 1024 + 4 * (size_t)A.mm_tiles * sizeof(BmRed) +
+                           4 * (size_t)A.mm_ks * sizeof(BmSrc);
+        const bool lz = A.lazy_out != 0;
+        switch (A.mm_ks) {
+#define BM_CASE(K)                                                                                             \
+    case K:                                                                                                    \
+        if (lz)                                                                                                \
+            hipLaunchKernelGGL((k_bconv_mma<K, true>), dim3((u32)grid), dim3(BCONV_MMA_THREADS), lds, s, A, x, \
+                               out, batch);                                                                    \
+        else                                                                                                   \
+            hipLaunchKernelGGL((k_bconv_mma<K, false>), dim3((u32)grid), dim3(BCONV_MMA_THREADS), lds, s, A,   \
+                               x, out, batch);                                                                 \
+        break;
+            BM_CASE(1) BM_CASE(2) BM_CASE(3) BM_CASE(4) BM_CASE(5) BM_CASE(6) BM_CASE(7) BM_CASE(8)
+#undef BM_CASE
+            default:
+                return fail(OFHE_ERR_STATE, "bconv: bad K-step count");
+        }
+        return post_launch();
+    }
     if (A.size_q <= BCONV_LIMB_QMAX && !generic)
         hipLaunchKernelGGL((k_bconv_limb<BCONV_PT>), dim3((u32)blocks), dim3(256), 0, s, A, x, out, batch);
     else
