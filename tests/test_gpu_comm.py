@@ -43,3 +43,18 @@ def test_comm_init_rejects_bad_ranks(hip):
         H.Comm(ctx, 0, 0, uid)
     with pytest.raises(H.MathError):
         H.Comm(ctx, 1, 0, uid[:16])
+
+
+def test_comm_init_times_out_without_peers(hip, monkeypatch):
+    """A communicator whose peers never arrive fails with an error after
+    OFHE_COMM_INIT_TIMEOUT_S instead of hanging (non-blocking init polled
+    against a deadline); shard.key_broadcaster then falls back on every rank."""
+    import time
+
+    H, ctx = hip
+    monkeypatch.setenv("OFHE_COMM_INIT_TIMEOUT_S", "3")
+    uid = H.comm_unique_id()
+    t0 = time.monotonic()
+    with pytest.raises(H.MathError, match="timed out"):
+        H.Comm(ctx, 2, 0, uid)
+    assert time.monotonic() - t0 < 60

@@ -14,9 +14,12 @@
 // every other entry point; nothing here synchronises.
 #include <rccl/rccl.h>
 
+#include <chrono>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <string>
+#include <thread>
 
 #include "internal.hpp"
 
@@ -31,6 +34,29 @@ struct ofhe_comm_s {
 namespace {
 int rccl_fail(const char* what, ncclResult_t r) {
     return ofhe::fail(OFHE_ERR_HIP, std::string(what) + ": " + ncclGetErrorString(r));
+}
+
+// The communicator is created non-blocking and polled against a deadline
+// (OFHE_COMM_INIT_TIMEOUT_S, default 120 s): a peer that never arrives makes
+// ofhe_hip_comm_init fail with an error instead of hanging the job, and the
+// caller falls back (shard.key_broadcaster agrees on the fallback across ranks).
+double init_timeout_s() {
+    const char* e = getenv("OFHE_COMM_INIT_TIMEOUT_S");
+    const double v = e ? atof(e) : 120.0;
+    return v > 0 ? v : 120.0;
+}
+// wait for a non-blocking communicator's pending call; ncclInProgress -> done or error
+ncclResult_t settle(ncclComm_t c, double timeout_s) {
+    const auto t0 = std::chrono::steady_clock::now();
+    for (;;) {
+        ncclResult_t st = ncclInProgress;
+        const ncclResult_t r = ncclCommGetAsyncError(c, &st);
+        if (r != ncclSuccess) return r;
+        if (st != ncclInProgress) return st;
+        const double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        if (dt > timeout_s) return ncclInProgress;
+        std::this_thread::sleep_for(std::chrono::microseconds(50));
+    }
 }
 }  // namespace
 
@@ -51,8 +77,15 @@ int ofhe_hip_comm_init(ofhe_ctx_t ctx, int nranks, int rank, const void* id, ofh
     ncclUniqueId u;
     std::memcpy(u.internal, id, sizeof(u.internal));
     ncclComm_t c = nullptr;
-    const ncclResult_t r = ncclCommInitRank(&c, nranks, u, rank);
-    if (r != ncclSuccess) return rccl_fail("ncclCommInitRank", r);
+    ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+    cfg.blocking = 0;
+    ncclResult_t r = ncclCommInitRankConfig(&c, nranks, u, rank, &cfg);
+    if (r == ncclInProgress) r = settle(c, init_timeout_s());
+    if (r != ncclSuccess) {
+        if (c) (void)ncclCommAbort(c);
+        if (r == ncclInProgress) return ofhe::fail(OFHE_ERR_HIP, "ncclCommInitRankConfig: timed out waiting for the peer ranks");
+        return rccl_fail("ncclCommInitRankConfig", r);
+    }
     ofhe_comm_s* s = new (std::nothrow) ofhe_comm_s();
     if (!s) {
         (void)ncclCommDestroy(c);
@@ -83,7 +116,8 @@ int ofhe_hip_bcast_evalkey(ofhe_comm_t c, uint64_t* key, size_t words, int root,
     HIPCHK(hipSetDevice(c->ctx->device));
     // u64 words as ncclUint64: in place (sendbuff == recvbuff), the root's
     // buffer is read, every other rank's is overwritten
-    const ncclResult_t r = ncclBroadcast(key, key, words, ncclUint64, root, c->comm, ofhe::pick(stream));
+    ncclResult_t r = ncclBroadcast(key, key, words, ncclUint64, root, c->comm, ofhe::pick(stream));
+    if (r == ncclInProgress) r = settle(c->comm, init_timeout_s());  // enqueue of a non-blocking comm
     if (r != ncclSuccess) return rccl_fail("ncclBroadcast", r);
     return OFHE_OK;
 }
