@@ -178,16 +178,40 @@ __device__ __forceinline__ u64 canon8(u64 x, u64 q) {  // [0, 8q) -> [0, q)
     x = csub_s(x, 2 * q);
     return csub_s(x, q);
 }
-// forward-transform output (any stage pattern) -> [0, q)
-template <bool SPQ>
-__device__ __forceinline__ u64 canon_fwd(u64 x, u64 q) {
-    if (SPQ && OFHE_THR) x = csub_s(x, 8 * q);  // [0, 2^(L+3) + 8q) -> [0, 8q + 8d)
-    if (OFHE_LAZY_FWD) x = csub_s(x, 8 * q);    // [0, 16q) -> [0, 8q)
-    return canon8(x, q);
-}
 __device__ __forceinline__ u64 canon4(u64 x, u64 q) {  // [0, 4q) -> [0, q)
     x = csub_s(x, 2 * q);
     return csub_s(x, q);
+}
+// Special prime q = 2^L - d (plan condition: d < 2^32 and 16 d < q): any
+// x < 2^(L+4) -> [0, q) with one quotient by shift.  qh = x >> L < 16,
+// r = (x mod 2^L) + qh d = x - qh q < 2^L + 15 d = q + 16 d < 2q, one
+// conditional subtract: 3 + 4 instructions against 12 (canon8) or 16 (canon_fwd).
+#ifndef OFHE_SPQ_CANON
+#define OFHE_SPQ_CANON 1
+#endif
+template <bool SPQ>
+__device__ __forceinline__ u64 canon_spq(u64 x, const Mod<SPQ>& M) {
+    const u32 qh = hi32(x) >> M.sh;
+    const u64 d = (1ull << (M.sh + 32)) - M.q;  // wave-uniform (scalar unit)
+    const u64 xm = pack(lo32(x), hi32(x) & ((1u << M.sh) - 1));
+    return csub_s(mad32(qh, lo32(d), xm), M.q);
+}
+template <bool SPQ>
+__device__ __forceinline__ u64 canon8m(u64 x, const Mod<SPQ>& M) {  // [0, 8q) -> [0, q)
+    return (SPQ && OFHE_SPQ_CANON) ? canon_spq(x, M) : canon8(x, M.q);
+}
+template <bool SPQ>
+__device__ __forceinline__ u64 canon4m(u64 x, const Mod<SPQ>& M) {  // [0, 4q) -> [0, q)
+    return (SPQ && OFHE_SPQ_CANON) ? canon_spq(x, M) : canon4(x, M.q);
+}
+// forward-transform output (any stage pattern) -> [0, q)
+template <bool SPQ>
+__device__ __forceinline__ u64 canon_fwd(u64 x, const Mod<SPQ>& M) {
+    if (SPQ && OFHE_SPQ_CANON && !OFHE_THR) return canon_spq(x, M);  // < 16q < 2^(L+4)
+    const u64 q = M.q;
+    if (SPQ && OFHE_THR) x = csub_s(x, 8 * q);  // [0, 2^(L+3) + 8q) -> [0, 8q + 8d)
+    if (OFHE_LAZY_FWD) x = csub_s(x, 8 * q);    // [0, 16q) -> [0, 8q)
+    return canon8(x, q);
 }
 
 // ---------------------------------------------------------------------------
@@ -281,7 +305,7 @@ __device__ __forceinline__ void dit_round3(u64 (&v)[16], const u64* dtw, const M
 // last step of every inverse: x * N^-1 psi^-j (the twist entry f) -> [0, q)
 template <bool SPQ>
 __device__ __forceinline__ u64 twist_out(u64 x, Tw f, const Mod<SPQ>& M) {
-    return canon4(shoup_lazy(x, f.w, f.wp, M), M.q);
+    return canon4m(shoup_lazy(x, f.w, f.wp, M), M);
 }
 
 // ---------------------------------------------------------------------------
@@ -543,7 +567,7 @@ __global__ __launch_bounds__(256, OFHE_KB_WAVES) void k_block(PlanArgs P, const 
         }
         if (!(MODE == MODE_FUSED && kMontFused)) {
 #pragma unroll
-            for (int k = 0; k < 16; k++) v[k] = canon_fwd<SPQ>(v[k], q);
+            for (int k = 0; k < 16; k++) v[k] = canon_fwd<SPQ>(v[k], M);
         }
         if (MODE == MODE_FWD_SUB) {
             u64 xx[16];
@@ -685,7 +709,6 @@ __global__ __launch_bounds__(16 * TCOLS_W, OFHE_KB_WAVES) void k_tcols(PlanArgs 
     const u64* x = src + (u64)b * P.sstride + inner;
     u64* y = dst + (u64)b * P.dstride + inner;
     const TowerConst tc = P.tc[t];
-    const u64 q = tc.q;
     const Mod<SPQ> M = load_mod<SPQ>(tc);
     const u32 h = tid / W, r = tid % W;
     const u32 L1 = tid, L2 = h * 16 * W + r;
@@ -728,7 +751,7 @@ __global__ __launch_bounds__(16 * TCOLS_W, OFHE_KB_WAVES) void k_tcols(PlanArgs 
             inv_round16_b(v, b8, itw, 1, M);
 #pragma unroll
             for (int k = 0; k < 16; k++)
-                st_s(y + (u64)(h + 16 * k) * S + r, b8[k] ? canon8(v[k], q) : canon4(v[k], q));
+                st_s(y + (u64)(h + 16 * k) * S + r, b8[k] ? canon8m(v[k], M) : canon4m(v[k], M));
         } else {
             inv_round16(v, itw, 16 + h, M);
 #pragma unroll
@@ -738,7 +761,7 @@ __global__ __launch_bounds__(16 * TCOLS_W, OFHE_KB_WAVES) void k_tcols(PlanArgs 
             for (int k = 0; k < 16; k++) v[k] = lds[L1 + 16 * W * k];
             inv_round16(v, itw, 1, M);
 #pragma unroll
-            for (int k = 0; k < 16; k++) st_s(y + (u64)(h + 16 * k) * S + r, canon4(v[k], q));
+            for (int k = 0; k < 16; k++) st_s(y + (u64)(h + 16 * k) * S + r, canon4m(v[k], M));
         }
     }
 }
@@ -772,7 +795,6 @@ __global__ __launch_bounds__(512) void k_tcols9(PlanArgs P, const u64* src, u64*
     const u64* x = src + (u64)b * P.sstride + inner;
     u64* y = dst + (u64)b * P.dstride + inner;
     const TowerConst tc = P.tc[t];
-    const u64 q = tc.q;
     const Mod<SPQ> M = load_mod<SPQ>(tc);
     const u32 h = tl / W, r = tl % W;
     u64* my = lds + hf * HALF;
@@ -829,10 +851,10 @@ __global__ __launch_bounds__(512) void k_tcols9(PlanArgs P, const u64* src, u64*
             const Tw w1 = ldtw(itw, 1);
 #pragma unroll
             for (int k = 0; k < 16; k++)
-                v[k] = canon4(shoup_lazy(other[L1 + 16 * W * k] + M.q4 - v[k], w1.w, w1.wp, M), q);
+                v[k] = canon4m(shoup_lazy(other[L1 + 16 * W * k] + M.q4 - v[k], w1.w, w1.wp, M), M);
         } else {
 #pragma unroll
-            for (int k = 0; k < 16; k++) v[k] = canon4(csub_s(v[k] + other[L1 + 16 * W * k], M.q4), q);
+            for (int k = 0; k < 16; k++) v[k] = canon4m(csub_s(v[k] + other[L1 + 16 * W * k], M.q4), M);
         }
 #pragma unroll
         for (int k = 0; k < 16; k++) st_s(y + (u64)(h + 16 * k) * S + r, v[k]);
@@ -913,7 +935,6 @@ __global__ __launch_bounds__(256) void k_cols(PlanArgs P, const u64* src, u64* d
     const u64* x = src + (u64)b * P.sstride + inner;
     u64* y = dst + (u64)b * P.dstride + inner;
     const TowerConst tc = P.tc[t];
-    const u64 q = tc.q;
     const Mod<SPQ> M = load_mod<SPQ>(tc);
     u64 v[CPT][E];
 #pragma unroll
@@ -935,13 +956,13 @@ __global__ __launch_bounds__(256) void k_cols(PlanArgs P, const u64* src, u64* d
 #pragma unroll
             for (int k = 0; k < E; k++)
 #pragma unroll
-                for (int c = 0; c < CPT; c++) v[c][k] = b8[k] ? canon8(v[c][k], q) : canon4(v[c][k], q);
+                for (int c = 0; c < CPT; c++) v[c][k] = b8[k] ? canon8m(v[c][k], M) : canon4m(v[c][k], M);
         } else {
             cols_inv<E, CPT>(v, P.itw + (u64)t * N * 2, M);
 #pragma unroll
             for (int k = 0; k < E; k++)
 #pragma unroll
-                for (int c = 0; c < CPT; c++) v[c][k] = canon4(v[c][k], q);
+                for (int c = 0; c < CPT; c++) v[c][k] = canon4m(v[c][k], M);
         }
     }
 #pragma unroll
@@ -989,7 +1010,7 @@ __global__ __launch_bounds__(256) void k_small(PlanArgs P, const u64* src, u64* 
             __syncthreads();
         }
         for (u32 i = threadIdx.x; i < N; i += blockDim.x) {
-            u64 x = canon_fwd<SPQ>(lds[i], q);
+            u64 x = canon_fwd<SPQ>(lds[i], M);
             if (MODE == MODE_FUSED) x = barrett_ref(x, bdat[off + i], q, tc.mu, tc.nshift);
             lds[i] = x;
         }

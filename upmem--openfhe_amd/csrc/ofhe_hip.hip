@@ -266,7 +266,10 @@ int ofhe_hip_plan_create(ofhe_ctx_t ctx, uint32_t log_n, uint32_t towers, const 
         c.mu = (u64)((((u128)1) << (2 * mb + 3)) / qt);  // ComputeMu, ubintnat.h:651-656
         c.nshift = mb - 2;
         // special prime q = 2^mb - d, d < 2^32: hi32(q) == 2^(mb-32) - 1
-        c.spq_sh = (mb >= 33 && (qt >> 32) == ((1ull << (mb - 32)) - 1)) ? mb - 32 : 0;
+        // and 16 d < q, d != 2^32 (canon_spq's single conditional subtract)
+        const bool spq = mb >= 33 && (qt >> 32) == ((1ull << (mb - 32)) - 1) && (u32)qt != 0 &&
+                         (((1ull << mb) - qt) << 4) < qt;
+        c.spq_sh = spq ? mb - 32 : 0;
         c.nq = 0 - qt;
         c.nq4 = 0 - 4 * qt;
         u64 inv = qt;  // q^-1 mod 2^64 by Newton iteration (q odd)
