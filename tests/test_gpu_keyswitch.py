@@ -155,6 +155,32 @@ def test_base_conversion_max_sums(hip, sq, reps):
     assert np.array_equal(host(out)[0], want)
 
 
+@pytest.mark.parametrize("sq", [3, 16])
+def test_base_conversion_special_primes(hip, sq):
+    """Targets that are all of the form 2^L - d (k_bconv_mma's shift fold,
+    bm_reduce<.., SPQ>): d = 1 and d = 2^32 - 1 at L = 60, and the smallest L
+    the host admits for a large d, with the same extreme inputs as
+    test_base_conversion_max_sums.  Expected values by Python integers."""
+    H, ctx = hip
+    import torch
+
+    log_n, n = 5, 32
+    q = [(1 << 60) - 1 - 2 * i for i in range(sq)]
+    p = [(1 << 60) - 1, (1 << 60) - (1 << 32) + 1, (1 << 58) - 12345, (1 << 55) - (1 << 23) + 5,
+         (1 << 54) - (1 << 26) + 1, (1 << 60) - 93, (1 << 59) - 55, (1 << 57) - 3]
+    bc = H.BaseConverter(ctx, log_n, q, p, [1] * sq, [pj - 1 for _ in q for pj in p])
+    rng = np.random.default_rng(100 + sq)
+    x = np.stack([np.full(n, qi - 1, np.uint64) for qi in q])
+    x[:, 1::2] = np.stack([rng.integers(0, qi, size=n // 2, dtype=np.uint64) for qi in q])
+    x[:, 2::4] = np.uint64(0x007F7F7F7F7F7F80)
+    dx = dev(x[None])
+    out = torch.zeros((1, len(p), n), dtype=torch.int64, device="cuda")
+    bc.switch(dx.data_ptr(), out.data_ptr(), 1, stream())
+    want = np.array([[sum(int(x[i, k]) * (pj - 1) for i in range(sq)) % pj for k in range(n)] for pj in p],
+                    np.uint64)
+    assert np.array_equal(host(out)[0], want)
+
+
 def test_keyswitch_inner_max_values(hip):
     """Inner product with every digit and key word m - 1 (the largest limb sums
     of the batch-stationary kernel), against the oracle."""

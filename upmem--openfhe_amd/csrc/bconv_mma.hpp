@@ -51,6 +51,9 @@ constexpr u32 BCONV_MMA_THREADS = 512;
 #ifndef OFHE_BCONV_MMA_PAIR
 #define OFHE_BCONV_MMA_PAIR 0  // two target tiles per MFMA round (interleaved chains): 15 % slower, not used
 #endif
+#ifndef OFHE_BCONV_MMA_SPQ
+#define OFHE_BCONV_MMA_SPQ 1  // special-prime reduction when every target allows it
+#endif
 #ifndef OFHE_BCONV_MMA_PF
 #define OFHE_BCONV_MMA_PF 1  // prefetch the next group's x
 #endif
@@ -100,12 +103,25 @@ __device__ __forceinline__ long long mad_i64(int a, int b, long long c) { return
 //   t  = H (2^60 mod p) - qh p + L'   with qh = single-word Shoup quotient
 //        (<= 1 short: H (2^60 mod p) - qh p in [0, 3p)), so t < 2^62.01
 //   r  = t - mulhi~(t, floor(2^64/p)) p in [0, 4p)   (as limb_reduce), then two csubs.
-template <bool LAZY>
+//
+// SPQ (every target p = 2^L - d, d < 2^32, with (2^(80-L) + 1) d + 2^48 + 2d
+// < 2^L, checked by the host): T' = H 2^L + L'' with H = hi_u >> (L - 32)
+// < 2^(80-L) and L'' < 2^L + 2^48, and T' == L'' + H d (mod p) with
+// L'' + H d < 2p: one v_mad_u64_u32 and at most one conditional subtract.
+// The table then holds d in r60 and (L - 32) | mask << 32 in r60p.
+template <bool LAZY, bool SPQ>
 __device__ __forceinline__ u64 bm_reduce(const int* C, const BmRed& R, const BmW& W) {
     const int x01 = C[0] + C[1] * 256, x23 = C[2] + C[3] * 256;
     const int x45 = C[4] + C[5] * 256, x67 = C[6] + C[7] * 256;
     const u64 lo_u = (u64)mad_i64(x23, W.w16, mad_i64(x01, W.w0, (long long)R.blo));
     const u64 hi_u = (u64)mad_i64(x67, W.w16, mad_i64(x45, W.w0, (long long)R.bhi));
+    if (SPQ) {
+        const u32 sh = lo32(R.r60p), mask = hi32(R.r60p);
+        const u32 H = (u32)(hi_u >> sh);
+        const u64 l2 = pack(lo32(lo_u), hi32(lo_u) + (lo32(hi_u) & mask));
+        const u64 r = mad32(H, lo32(R.r60), l2);  // < 2p
+        return LAZY ? r : csub(r, R.p);
+    }
     const u32 H = (u32)(hi_u >> 28);
     const u32 qh = hi32(mad32(H, hi32(R.r60p), (u64)__umulhi(H, lo32(R.r60p))));
     const u32 lh = hi32(lo_u) + (lo32(hi_u) & 0x0FFFFFFFu) + H * hi32(R.r60) + qh * hi32(R.np);
@@ -122,7 +138,7 @@ __device__ __forceinline__ u64 bm_reduce(const int* C, const BmRed& R, const BmW
 // One wave = 32 coefficients (a group of one batch entry, N >= 32); the block's
 // waves walk the groups grid-stride and share the fragment table in LDS.
 // KS = K-steps of 4 source towers (size_q <= 4 KS).
-template <int KS, bool LAZY>
+template <int KS, bool LAZY, bool SPQ>
 __global__ __launch_bounds__(BCONV_MMA_THREADS, OFHE_BCONV_MMA_WAVES) void k_bconv_mma(BconvArgs A, const u64* __restrict__ x,
                                                                  u64* __restrict__ out, u32 batch) {
     extern __shared__ __attribute__((aligned(16))) unsigned char bm_lds[];
@@ -191,7 +207,7 @@ __global__ __launch_bounds__(BCONV_MMA_THREADS, OFHE_BCONV_MMA_WAVES) void k_bco
 #pragma unroll
                     for (int k = 0; k < 8; k++) C[k] = acc[8 * u + k];
                     const u32 jo = j >= A.gap_at ? j + A.gap : j;
-                    st_s(ob + (u64)jo * N, bm_reduce<LAZY>(C, red[j], W));
+                    st_s(ob + (u64)jo * N, bm_reduce<LAZY, SPQ>(C, red[j], W));
                 }
             }
         };

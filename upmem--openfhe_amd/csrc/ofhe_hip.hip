@@ -791,7 +791,7 @@ T* pred_of(T* qhlimb, u32 qrows, u32 ppad) { return qhlimb + (size_t)qrows * ppa
 // [tiles][ks][64 lanes][16 int8], then BmRed[4 tiles], then BmSrc[4 ks].
 // qhinv: [size_q][2] (canonical QHatInvModq, Shoup precon); qhmodp: [size_q][size_p], canonical.
 static bool bconv_mma_table(u32 size_q, u32 size_p, const u64* q, const u64* p, const u64* qhinv,
-                            const u64* qhmodp, std::vector<unsigned char>& tab, u32& tiles, u32& ks) {
+                            const u64* qhmodp, std::vector<unsigned char>& tab, u32& tiles, u32& ks, bool& spq) {
     ks = (size_q + 3) / 4;
     tiles = (size_p + 3) / 4;
     const size_t fbytes = (size_t)tiles * ks * 1024;
@@ -817,6 +817,14 @@ static bool bconv_mma_table(u32 size_q, u32 size_p, const u64* q, const u64* p, 
                 }
             }
     BmRed* red = reinterpret_cast<BmRed*>(tab.data() + fbytes);
+    // special-prime reduction (bm_reduce<.., SPQ>) when every target allows it
+    spq = OFHE_BCONV_MMA_SPQ != 0;
+    for (u32 j = 0; j < size_p && spq; j++) {
+        const unsigned L = msb64(p[j]);
+        const u64 d = L >= 33 && L <= 60 ? (1ull << L) - p[j] : 0;
+        spq = d != 0 && d < (1ull << 32) &&
+              (((u128)1 << (80 - L)) + 1) * d + ((u128)1 << 48) + 2 * (u128)d < ((u128)1 << L);
+    }
     for (u32 j = 0; j < size_p; j++) {
         BmRed& R = red[j];
         u64 lr[3];
@@ -831,6 +839,11 @@ static bool bconv_mma_table(u32 size_q, u32 size_p, const u64* q, const u64* p, 
         R.bhi = (u64)(bias >> 32) - (1ull << 15);
         R.blo = (u64)(bias & 0xFFFFFFFFull) + (1ull << 47);
         R.p2 = 2 * p[j];
+        if (spq) {
+            const unsigned L = msb64(p[j]);
+            R.r60 = (1ull << L) - p[j];                               // d
+            R.r60p = (u64)(L - 32) | ((u64)((1u << (L - 32)) - 1) << 32);  // shift | mask << 32
+        }
     }
     BmSrc* src = reinterpret_cast<BmSrc*>(red + 4 * tiles);
     for (u32 i = 0; i < size_q; i++) src[i] = BmSrc{q[i], qhinv[2 * i], qhinv[2 * i + 1], 0};
@@ -880,10 +893,11 @@ int ofhe_hip_bconv_create(ofhe_ctx_t ctx, uint32_t log_n, uint32_t size_q, uint3
     }
     // the matrix-core kernel's table (bconv_mma.hpp), appended 16-byte aligned
     u32 mm_tiles = 0, mm_ks = 0;
+    bool mm_spq = false;
     size_t mm_off = 0;
     {
         std::vector<unsigned char> tab;
-        if (bconv_mma_table(size_q, size_p, q, p, qhinv, qhmodp, tab, mm_tiles, mm_ks)) {
+        if (bconv_mma_table(size_q, size_p, q, p, qhinv, qhmodp, tab, mm_tiles, mm_ks, mm_spq)) {
             mm_off = (h.size() + 1) & ~(size_t)1;
             h.resize(mm_off + tab.size() / 8);
             std::memcpy(h.data() + mm_off, tab.data(), tab.size());
@@ -919,6 +933,7 @@ int ofhe_hip_bconv_create(ofhe_ctx_t ctx, uint32_t log_n, uint32_t size_q, uint3
     A.mm_tab = mm_tiles ? (const void*)(b->d_mem + mm_off) : nullptr;
     A.mm_tiles = mm_tiles;
     A.mm_ks = mm_ks;
+    A.mm_spq = mm_spq ? 1 : 0;
     *out = b;
     return OFHE_OK;
 }
@@ -947,19 +962,21 @@ int bconv_run(const BconvArgs& A, const u64* x, u64* out, u32 batch, hipStream_t
         if (grid > cap) grid = cap;
         const size_t lds = (size_t)A.mm_tiles * A.mm_ks * 1024 + 4 * (size_t)A.mm_tiles * sizeof(BmRed) +
                            4 * (size_t)A.mm_ks * sizeof(BmSrc);
-        const bool lz = A.lazy_out != 0;
+        const int var = (A.lazy_out ? 1 : 0) | (A.mm_spq ? 2 : 0);
         switch (A.mm_ks) {
-#define BM_CASE(K)                                                                                             \
-    case K:                                                                                                    \
-        if (lz)                                                                                                \
-            hipLaunchKernelGGL((k_bconv_mma<K, true>), dim3((u32)grid), dim3(BCONV_MMA_THREADS), lds, s, A, x, \
-                               out, batch);                                                                    \
-        else                                                                                                   \
-            hipLaunchKernelGGL((k_bconv_mma<K, false>), dim3((u32)grid), dim3(BCONV_MMA_THREADS), lds, s, A,   \
-                               x, out, batch);                                                                 \
+#define BM_LAUNCH(K, LZ, SP)                                                                                   \
+    hipLaunchKernelGGL((k_bconv_mma<K, LZ, SP>), dim3((u32)grid), dim3(BCONV_MMA_THREADS), lds, s, A, x, out, \
+                       batch)
+#define BM_CASE(K)                                 \
+    case K:                                        \
+        if (var == 0) BM_LAUNCH(K, false, false);  \
+        if (var == 1) BM_LAUNCH(K, true, false);   \
+        if (var == 2) BM_LAUNCH(K, false, true);   \
+        if (var == 3) BM_LAUNCH(K, true, true);    \
         break;
             BM_CASE(1) BM_CASE(2) BM_CASE(3) BM_CASE(4) BM_CASE(5) BM_CASE(6) BM_CASE(7) BM_CASE(8)
 #undef BM_CASE
+#undef BM_LAUNCH
             default:
                 return fail(OFHE_ERR_STATE, "bconv: bad K-step count");
         }
