@@ -126,20 +126,23 @@ def test_approx_mod_down(hip, log_n, sq, sp, generic, t):
     assert np.array_equal(host(out), K.approx_mod_down(x, q, rq, p, rp, t))
 
 
-@pytest.mark.parametrize("sq,reps", [(1, 1), (7, 1), (16, 1), (17, 1), (32, 1), (33, 1), (16, 8)])
-def test_base_conversion_max_sums(hip, sq, reps):
+@pytest.mark.parametrize("sq,reps,log_n", [(1, 1, 5), (7, 1, 5), (16, 1, 5), (17, 1, 5), (32, 1, 5), (33, 1, 5),
+                                           (64, 1, 5), (16, 8, 5), (40, 24, 5), (65, 1, 5), (7, 1, 4)])
+def test_base_conversion_max_sums(hip, sq, reps, log_n):
     """Extreme sums for every base-conversion kernel: inputs q_i - 1 (q_i up
     to 2^60 - 1) and 0x007F7F7F7F7F7F80 (seven signed base-256 digits of
     -128 in the matrix-core kernel's digit split), QHatInvModq = 1 and every
     QHatModp entry p_j - 1, for output moduli from 2 to 2^60 - 1 (powers of
-    two included).  size_q <= 32 with a small target set runs k_bconv_mma
-    (K-steps 1, 2, 4, 5, 8), size_q = 33 the 128-bit k_bconv, and 16 sources
-    into 72 targets (fragment table above the LDS budget) k_bconv_limb.
-    Expected values by Python integers: out_j = sum_i x_i (p_j - 1) mod p_j."""
+    two included).  k_bconv_mma for size_q <= 64: K-steps 1, 2, 4, 5, 8 and
+    the wide partial sums at 10 (33 sources) and 16 (64); 16 -> 72 and
+    40 -> 216 targets run in several target chunks (blockIdx.y).  size_q = 65
+    runs the 128-bit k_bconv, N = 16 (below one 32-coefficient group)
+    k_bconv_limb.  Expected values by Python integers:
+    out_j = sum_i x_i (p_j - 1) mod p_j."""
     H, ctx = hip
     import torch
 
-    log_n, n = 5, 32
+    n = 1 << log_n
     q = [(1 << 60) - 1 - 2 * i for i in range(sq)]
     p = [2, 3, 1 << 31, (1 << 32) + 15, (1 << 45) + 7, (1 << 59) + 1, (1 << 60) - 1, 1 << 59, 97] * reps
     bc = H.BaseConverter(ctx, log_n, q, p, [1] * sq, [pj - 1 for _ in q for pj in p])
@@ -150,8 +153,8 @@ def test_base_conversion_max_sums(hip, sq, reps):
     dx = dev(x[None])
     out = torch.zeros((1, len(p), n), dtype=torch.int64, device="cuda")
     bc.switch(dx.data_ptr(), out.data_ptr(), 1, stream())
-    want = np.array([[sum(int(x[i, k]) * (pj - 1) for i in range(sq)) % pj for k in range(n)] for pj in p],
-                    np.uint64)
+    xs = [sum(int(x[i, k]) for i in range(sq)) for k in range(n)]
+    want = np.array([[xs[k] * (pj - 1) % pj for k in range(n)] for pj in p], np.uint64)
     assert np.array_equal(host(out)[0], want)
 
 
@@ -220,6 +223,7 @@ KS_CASES = [
     (16, 6, 2, 3, False),   # N = 2^16 (8|8 split transforms)
     (5, 8, 2, 4, False),    # beta = 4 (largest batch-stationary inner product)
     (5, 10, 2, 5, False),   # beta = 5 (generic inner product kernel)
+    (10, 40, 4, 1, False),  # dnum = 1: a 40-tower digit (matrix-core conversion, wide partial sums)
 ]
 
 

@@ -176,6 +176,7 @@ struct BconvArgs {
     u32 gap_at, gap;      // output tower j >= gap_at is written at j + gap (key-switch digit slot)
     const void* mm_tab;   // k_bconv_mma fragment table + constants (bconv_mma.hpp), or null
     u32 mm_tiles, mm_ks;  // its target tiles (4 towers) and K-steps (4 source towers)
+    u32 mm_tpc;           // target tiles per block (blockIdx.y chunk) that fit the LDS budget
     u32 lazy_out;         // internal callers: outputs in [0, 4p) (a forward NTT follows)
     u32 mm_spq;           // k_bconv_mma: every target a special prime (bm_reduce's shift fold)
 };

@@ -790,16 +790,27 @@ T* pred_of(T* qhlimb, u32 qrows, u32 ppad) { return qhlimb + (size_t)qrows * ppa
 // k_bconv_mma's LDS image (bconv_mma.hpp): A-operand fragments
 // [tiles][ks][64 lanes][16 int8], then BmRed[4 tiles], then BmSrc[4 ks].
 // qhinv: [size_q][2] (canonical QHatInvModq, Shoup precon); qhmodp: [size_q][size_p], canonical.
+// A chunk of tpc target tiles per block (blockIdx.y) keeps the LDS image of
+// one block within BCONV_MMA_LDS_MAX for any size_p.
+static u32 bconv_mma_lds(u32 tpc, u32 ks) { return tpc * (ks * 1024 + 4 * (u32)sizeof(BmRed)) + 4 * ks * (u32)sizeof(BmSrc); }
 static bool bconv_mma_table(u32 size_q, u32 size_p, const u64* q, const u64* p, const u64* qhinv,
-                            const u64* qhmodp, std::vector<unsigned char>& tab, u32& tiles, u32& ks, bool& spq) {
+                            const u64* qhmodp, std::vector<unsigned char>& tab, u32& tiles, u32& ks, u32& tpc,
+                            bool& spq) {
     ks = (size_q + 3) / 4;
+    if (ks > 8) ks = (ks + 1) & ~1u;  // instantiated K-step counts: 1..8, 10, 12, 14, 16 (zero-padded sources)
     tiles = (size_p + 3) / 4;
-    const size_t fbytes = (size_t)tiles * ks * 1024;
-    const size_t bytes = fbytes + 4 * (size_t)tiles * sizeof(BmRed) + 4 * (size_t)ks * sizeof(BmSrc);
-    if (size_q > BCONV_MMA_QMAX || bytes > BCONV_MMA_LDS_MAX) {
+    tpc = 0;
+    if (size_q > BCONV_MMA_QMAX) {
         tiles = ks = 0;
         return false;
     }
+    while (tpc < tiles && bconv_mma_lds(tpc + 1, ks) <= BCONV_MMA_LDS_MAX) tpc++;
+    if (tpc == 0) {
+        tiles = ks = 0;
+        return false;
+    }
+    const size_t fbytes = (size_t)tiles * ks * 1024;
+    const size_t bytes = fbytes + 4 * (size_t)tiles * sizeof(BmRed) + 4 * (size_t)ks * sizeof(BmSrc);
     tab.assign(bytes, 0);
     // h_{(i,a),j} = 2^(8a) QHatModp_{i,j} mod p_j, as signed base-256 digits
     for (u32 t = 0; t < tiles; t++)
@@ -823,7 +834,7 @@ static bool bconv_mma_table(u32 size_q, u32 size_p, const u64* q, const u64* p, 
         const unsigned L = msb64(p[j]);
         const u64 d = L >= 33 && L <= 60 ? (1ull << L) - p[j] : 0;
         spq = d != 0 && d < (1ull << 32) &&
-              (((u128)1 << (80 - L)) + 1) * d + ((u128)1 << 48) + 2 * (u128)d < ((u128)1 << L);
+              (((u128)1 << (81 - L)) + 1) * d + ((u128)1 << 49) + 2 * (u128)d < ((u128)1 << L);
     }
     for (u32 j = 0; j < size_p; j++) {
         BmRed& R = red[j];
@@ -834,10 +845,10 @@ static bool bconv_mma_table(u32 size_q, u32 size_p, const u64* q, const u64* p, 
         R.r60 = lr[0];
         R.r60p = lr[1];
         R.mu1 = lr[2];
-        const u128 k = (((u128)1 << 79) + p[j] - 1) / p[j];
-        const u128 bias = k * p[j];
-        R.bhi = (u64)(bias >> 32) - (1ull << 15);
-        R.blo = (u64)(bias & 0xFFFFFFFFull) + (1ull << 47);
+        const u128 k = (((u128)1 << 80) + p[j] - 1) / p[j];
+        const u128 bias = k * p[j];  // in [2^80, 2^80 + p)
+        R.bhi = (u64)(bias >> 32) - (1ull << 16);
+        R.blo = (u64)(bias & 0xFFFFFFFFull) + (1ull << 48);
         R.p2 = 2 * p[j];
         if (spq) {
             const unsigned L = msb64(p[j]);
@@ -892,12 +903,12 @@ int ofhe_hip_bconv_create(ofhe_ctx_t ctx, uint32_t log_n, uint32_t size_q, uint3
         limb_red_consts(p[j], pred_of(qhlimb, qrows, ppad) + 3 * j);
     }
     // the matrix-core kernel's table (bconv_mma.hpp), appended 16-byte aligned
-    u32 mm_tiles = 0, mm_ks = 0;
+    u32 mm_tiles = 0, mm_ks = 0, mm_tpc = 0;
     bool mm_spq = false;
     size_t mm_off = 0;
     {
         std::vector<unsigned char> tab;
-        if (bconv_mma_table(size_q, size_p, q, p, qhinv, qhmodp, tab, mm_tiles, mm_ks, mm_spq)) {
+        if (bconv_mma_table(size_q, size_p, q, p, qhinv, qhmodp, tab, mm_tiles, mm_ks, mm_tpc, mm_spq)) {
             mm_off = (h.size() + 1) & ~(size_t)1;
             h.resize(mm_off + tab.size() / 8);
             std::memcpy(h.data() + mm_off, tab.data(), tab.size());
@@ -933,6 +944,7 @@ int ofhe_hip_bconv_create(ofhe_ctx_t ctx, uint32_t log_n, uint32_t size_q, uint3
     A.mm_tab = mm_tiles ? (const void*)(b->d_mem + mm_off) : nullptr;
     A.mm_tiles = mm_tiles;
     A.mm_ks = mm_ks;
+    A.mm_tpc = mm_tpc;
     A.mm_spq = mm_spq ? 1 : 0;
     *out = b;
     return OFHE_OK;
@@ -957,16 +969,17 @@ int bconv_run(const BconvArgs& A, const u64* x, u64* out, u32 batch, hipStream_t
     if (OFHE_BCONV_MMA && A.mm_tab && A.log_n >= 5 && !generic && !limb) {
         const u64 groups = total >> 5;
         const u32 wpb = BCONV_MMA_THREADS / 64;
-        u64 grid = (groups + wpb - 1) / wpb;
-        const u64 cap = 256ull * BCONV_MMA_BLOCKS_PER_CU;
-        if (grid > cap) grid = cap;
-        const size_t lds = (size_t)A.mm_tiles * A.mm_ks * 1024 + 4 * (size_t)A.mm_tiles * sizeof(BmRed) +
-                           4 * (size_t)A.mm_ks * sizeof(BmSrc);
+        const u32 chunks = (A.mm_tiles + A.mm_tpc - 1) / A.mm_tpc;
+        u64 gx = (groups + wpb - 1) / wpb;
+        u64 cap = 256ull * BCONV_MMA_BLOCKS_PER_CU / chunks;  // about BPC resident blocks per CU in all
+        if (cap < 1) cap = 1;
+        if (gx > cap) gx = cap;
+        const size_t lds = bconv_mma_lds(A.mm_tpc, A.mm_ks);
         const int var = (A.lazy_out ? 1 : 0) | (A.mm_spq ? 2 : 0);
+        const dim3 grid((u32)gx, chunks);
         switch (A.mm_ks) {
-#define BM_LAUNCH(K, LZ, SP)                                                                                   \
-    hipLaunchKernelGGL((k_bconv_mma<K, LZ, SP>), dim3((u32)grid), dim3(BCONV_MMA_THREADS), lds, s, A, x, out, \
-                       batch)
+#define BM_LAUNCH(K, LZ, SP) \
+    hipLaunchKernelGGL((k_bconv_mma<K, LZ, SP>), grid, dim3(BCONV_MMA_THREADS), lds, s, A, x, out, batch)
 #define BM_CASE(K)                                 \
     case K:                                        \
         if (var == 0) BM_LAUNCH(K, false, false);  \
@@ -975,6 +988,7 @@ int bconv_run(const BconvArgs& A, const u64* x, u64* out, u32 batch, hipStream_t
         if (var == 3) BM_LAUNCH(K, true, true);    \
         break;
             BM_CASE(1) BM_CASE(2) BM_CASE(3) BM_CASE(4) BM_CASE(5) BM_CASE(6) BM_CASE(7) BM_CASE(8)
+            BM_CASE(10) BM_CASE(12) BM_CASE(14) BM_CASE(16)
 #undef BM_CASE
 #undef BM_LAUNCH
             default:
