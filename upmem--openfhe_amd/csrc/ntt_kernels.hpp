@@ -480,6 +480,24 @@ __device__ __forceinline__ void wave_stage_in(const u64* wsrc, u64* lds, u32 tid
     for (int k = 0; k < 16; k++) out[k] = lds[tid * 17 + k];
     __builtin_amdgcn_wave_barrier();
 }
+// wave_stage_in whose first NPRE 16-byte loads were issued earlier (pre[]),
+// so their HBM latency overlaps the caller's compute
+template <int NPRE>
+__device__ __forceinline__ void wave_stage_in_pre(const u64* wsrc, u64* lds, u32 tid, const u64x2 (&pre)[NPRE > 0 ? NPRE : 1],
+                                                  u64 (&out)[16]) {
+    const u32 lane = tid & 63, base = (tid >> 6) * 1024;
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+        const u64x2 v = k < NPRE ? pre[k < NPRE ? k : 0] : ld2_s(wsrc + 128 * k + 2 * lane);
+        const u32 p = base + 128 * k + 2 * lane;
+        lds[lds_pad(p)] = v.x;
+        lds[lds_pad(p) + 1] = v.y;
+    }
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int k = 0; k < 16; k++) out[k] = lds[tid * 17 + k];
+    __builtin_amdgcn_wave_barrier();
+}
 __device__ __forceinline__ void wave_stage_out(const u64 (&v)[16], u64* lds, u32 tid, u64* wdst) {
     const u32 lane = tid & 63, base = (tid >> 6) * 1024;
 #pragma unroll
@@ -500,6 +518,9 @@ __device__ __forceinline__ void wave_stage_out(const u64 (&v)[16], u64* lds, u32
 // forward (canonical out), inverse (first 12 inverse stages), or the fused
 // forward -> Hadamard -> inverse pipeline.
 // ---------------------------------------------------------------------------
+#ifndef OFHE_B_PF
+#define OFHE_B_PF 8  // early second-operand loads in the fused / forward-subtract block pass (0..8)
+#endif
 #ifndef OFHE_KB_WAVES
 #define OFHE_KB_WAVES 4
 #endif
@@ -555,6 +576,14 @@ __global__ __launch_bounds__(256, OFHE_KB_WAVES) void k_block(PlanArgs P, const 
         // round 3: st = 1, p = 16 tid + k
 #pragma unroll
         for (int k = 0; k < 16; k++) v[k] = lds[L3 + k];
+        // the second operand (the fused pipeline's Hadamard b, ModDown's x):
+        // the first OFHE_B_PF of its 8 wave-coalesced 16-byte loads go out
+        // now, so their HBM latency hides under round 3 (same-process A/B,
+        // batch 256: fused block pass 1.740 -> 1.673 ms, VGPRs unchanged)
+        constexpr int BPF = ((MODE == MODE_FUSED && OFHE_COAL_B) || MODE == MODE_FWD_SUB) ? OFHE_B_PF : 0;
+        u64x2 bpre[BPF > 0 ? BPF : 1];
+#pragma unroll
+        for (int k = 0; k < BPF; k++) bpre[k] = ld2_s(bdat + boff + (tid >> 6) * 1024 + 128 * k + 2 * (tid & 63));
         if (OFHE_TW3) {
             const u64* tw3 = P.tw3 + (u64)t * (N / 16) * 30;
             const u32 U = N >> 4, u = g * 256 + tid;
@@ -571,7 +600,7 @@ __global__ __launch_bounds__(256, OFHE_KB_WAVES) void k_block(PlanArgs P, const 
         }
         if (MODE == MODE_FWD_SUB) {
             u64 xx[16];
-            wave_stage_in(bdat + boff + (tid >> 6) * 1024, lds, tid, xx);
+            wave_stage_in_pre<BPF>(bdat + boff + (tid >> 6) * 1024, lds, tid, bpre, xx);
             const u64 sc = P.scal[3 * t + 1], scp = P.scal[3 * t + 2];
 #pragma unroll
             for (int k = 0; k < 16; k++) {
@@ -594,7 +623,7 @@ __global__ __launch_bounds__(256, OFHE_KB_WAVES) void k_block(PlanArgs P, const 
         // Hadamard with b (evaluation form), NativeVectorT::ModMulNoCheckEq
         if (OFHE_COAL_B) {
             u64 bb[16];
-            wave_stage_in(bdat + boff + (tid >> 6) * 1024, lds, tid, bb);
+            wave_stage_in_pre<BPF>(bdat + boff + (tid >> 6) * 1024, lds, tid, bpre, bb);
             if (kMontFused) {
 #pragma unroll
                 for (int k = 0; k < 16; k++) v[k] = mont_mul(v[k], bb[k], q, tc.qinv);  // (0, 2q)
