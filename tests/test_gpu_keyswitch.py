@@ -184,6 +184,33 @@ def test_base_conversion_special_primes(hip, sq):
     assert np.array_equal(host(out)[0], want)
 
 
+@pytest.mark.parametrize("seed", range(8))
+def test_base_conversion_random_shapes(hip, seed):
+    """Seeded random ApproxSwitchCRTBasis shapes against the oracle
+    (oracle/keyswitch.py, the reference's loop): 1..64 source towers, 1..90
+    targets, special and generic moduli mixed or not, N = 2^5..2^8, batch
+    1..3 -- every K-step count, target chunking and both reduction forms of
+    k_bconv_mma, with the reference's own QHatInvModq / QHatModp tables."""
+    H, ctx = hip
+    import torch
+
+    rng = np.random.default_rng(1000 + seed)
+    log_n = int(rng.integers(5, 9))
+    n = 1 << log_n
+    sq, sp, batch = int(rng.integers(1, 65)), int(rng.integers(1, 91)), int(rng.integers(1, 4))
+    special = seed % 2 == 0
+    q, _, p, _ = (_bases if special else _generic_bases)(log_n, sq, sp)
+    if seed % 4 == 2:  # one generic target among special ones: the generic reduction for all
+        p = list(p[:-1]) + [_generic_bases(log_n, 0, 1)[2][0]]
+    qhinv, qhmodp = K.switch_tables(q, p)
+    bc = H.BaseConverter(ctx, log_n, q, p, qhinv, [v for row in qhmodp for v in row])
+    x = _uniform(rng, batch, q, n)
+    dx = dev(x)
+    out = torch.zeros((batch, sp, n), dtype=torch.int64, device="cuda")
+    bc.switch(dx.data_ptr(), out.data_ptr(), batch, stream())
+    assert np.array_equal(host(out), K._switch_basis(x, q, p, qhinv, qhmodp))
+
+
 def test_keyswitch_inner_max_values(hip):
     """Inner product with every digit and key word m - 1 (the largest limb sums
     of the batch-stationary kernel), against the oracle."""
