@@ -405,3 +405,37 @@ def test_stream_ordered_alloc_and_zero(hip):
     s.synchronize()
     h = out.cpu().numpy()
     assert not h[: n // 2].any() and np.array_equal(h[n // 2:], np.arange(n // 2, n))
+
+
+@pytest.mark.parametrize("batch,edge", [(1, False), (17, False), (150, False), (3, True)])
+def test_block_mma_vs_oracle(hip, O, monkeypatch, batch, edge):
+    """N = 2^16 fused pipeline with the matrix-core block pass (k_block_mma,
+    csrc/ntt_mma.hpp): batches of 1, 17 (one partial iteration of 16) and 150
+    (two workgroup chunks of 128, the second ragged) equal the oracle and the
+    butterfly block pass (k_block, the default); edge = all-(q-1) inputs.
+    k_block_mma is opt-in (OFHE_NTT_MMA=1; DESIGN.md, rejected variants)."""
+    import torch
+
+    H, ctx = hip
+    log_n, T = 16, 2
+    n = 1 << log_n
+    qs, rs = O.moduli_chain(log_n, T)
+    tb = O.Tables(n, qs, rs)
+    if edge:
+        a = np.broadcast_to(np.array(qs, np.uint64)[None, :, None] - np.uint64(1), (batch, T, n)).copy()
+        b = a.copy()
+    else:
+        a = O.uniform_dcrt(batch, T, n, qs, 500 + batch)
+        b = O.uniform_dcrt(batch, T, n, qs, 600 + batch)
+    outs = []
+    for env in ("1", "0"):
+        monkeypatch.setenv("OFHE_NTT_MMA", env)
+        plan = H.NTTPlan(ctx, log_n, qs, rs)
+        xa, xb = dev(a), dev(b)
+        xc = torch.empty_like(xa)
+        plan.ntt_mul_intt(xa.data_ptr(), xb.data_ptr(), xc.data_ptr(), batch, stream())
+        outs.append(host(xc))
+        plan.close()
+    assert np.array_equal(outs[0], outs[1])
+    sel = slice(None) if batch <= 17 else [0, 127, 128, batch - 1]
+    assert np.array_equal(outs[0][sel], O.ntt_mul_intt(a[sel], b[sel], tb))

@@ -114,6 +114,11 @@ struct ofhe_plan_s {
     hipStream_t st[2] = {nullptr, nullptr};
     hipEvent_t ev_fork = nullptr, ev_join[2] = {nullptr, nullptr};
     std::mutex fork_mu;  // guards st / ev_* (plan_tune, the two-stream pipeline)
+    // k_block_mma (ntt_mma.hpp): F_i / V_i fragments per (tower, group) and the
+    // per-tower reduction constants, built on the first fused call
+    void* d_nm = nullptr;
+    int nm_state = 0;  // 0 not built, 1 ready, -1 not applicable
+    std::mutex nm_mu;
 };
 
 struct ofhe_bconv_s {

@@ -17,6 +17,7 @@
 #include <thread>
 
 #include "internal.hpp"
+#include "ntt_mma.hpp"
 
 using namespace ofhe;
 
@@ -293,6 +294,12 @@ int ofhe_hip_plan_create(ofhe_ctx_t ctx, uint32_t log_n, uint32_t towers, const 
     for (u32 t = 0; t < towers; t++) p->spq = p->spq && tc[t].spq_sh != 0;
     if (getenv("OFHE_NO_SPQ")) p->spq = false;  // A/B switch for tests and timing
     p->split8 = split8;
+    {
+        // opt-in (OFHE_NTT_MMA=1): k_block_mma measured 1.7x slower than
+        // k_block at its 2 waves per SIMD (rejected variants)
+        const char* nm = getenv("OFHE_NTT_MMA");
+        if (!nm || atoi(nm) == 0) p->nm_state = -1;
+    }
     hipError_t e = hipSetDevice(ctx->device);
     if (e == hipSuccess) e = hipMalloc(&p->d_tc, sizeof(TowerConst) * towers);
     if (e == hipSuccess) e = hipMalloc(&p->d_tw, sizeof(u64) * 2 * TN);
@@ -368,6 +375,7 @@ int ofhe_hip_plan_destroy(ofhe_plan_t p) {
     (void)hipFree(p->d_dtw);
     (void)hipFree(p->d_twist);
     (void)hipFree(p->d_twist_r);
+    (void)hipFree(p->d_nm);
     delete p;
     return OFHE_OK;
 }
@@ -606,6 +614,149 @@ int ofhe_hip_ntt_inv_range(ofhe_plan_t p, uint32_t t0, uint32_t count, const uin
     return plan_ntt_range(p, true, t0, count, src, dst, src_stride, dst_stride, batch, pick(stream));
 }
 
+// ---------------------------------------------------------------------------
+// k_block_mma (ntt_mma.hpp): per tower t and group i the two 16 x 16 maps of
+// the block pass that do not depend on the column, as A-operand fragments of
+// v_mfma_i32_32x32x32_i8 in k_bconv_mma's layout (bconv_mma_table):
+//   F_i  forward CT stages m = 256 .. 2048 on elements i 256 + 16 j (column 0;
+//        every column has the same map), Table[m + e / (2t)];
+//   V_i  GS stages t = 16 .. 128, TableI[m + e / (2t)], times N^-1 2^64 (the
+//        2^64 cancels the Montgomery Hadamard's 2^-64).
+// Opt-in (OFHE_NTT_MMA=1 at plan creation): built on the first fused call of
+// a special-prime N = 2^16 plan (8 MiB per tower); never for other plans or a
+// modulus outside bm_reduce<SPQ>'s range.
+// ---------------------------------------------------------------------------
+#ifndef OFHE_NM_CHUNK
+#define OFHE_NM_CHUNK 128  // polynomials per workgroup (the batch loop of one group)
+#endif
+static bool nm_ready(ofhe_plan_t p) {
+    std::lock_guard<std::mutex> lk(p->nm_mu);
+    if (p->nm_state) return p->nm_state > 0;
+    p->nm_state = -1;
+    if (p->log_n != 16 || !p->spq || !p->split8) return false;
+    const u32 T = p->towers, N = 1u << 16;
+    for (u32 t = 0; t < T; t++) {
+        const u64 q = p->q[t];
+        const unsigned L = msb64(q);
+        const u64 d = (1ull << L) - q;
+        if (!(L >= 33 && d < (1ull << 32) && (((u128)1 << (81 - L)) + 1) * d + ((u128)1 << 49) + 2 * (u128)d < ((u128)1 << L)))
+            return false;
+    }
+    const size_t per_group = 2 * (size_t)NM_FRAG * 16;  // bytes
+    const size_t fbytes = (size_t)T * 256 * per_group;
+    std::vector<unsigned char> tab(fbytes + (size_t)T * sizeof(BmRed));
+    BmRed* red = reinterpret_cast<BmRed*>(tab.data() + fbytes);
+    auto build = [&](u32 t) {
+        const u64 q = p->q[t];
+        const u64* Tb = &p->tab[(size_t)t * N];
+        const u64* TI = &p->itab[(size_t)t * N];
+        const u64 scale = mulmod(p->ninv[t], (u64)(((u128)1 << 64) % q), q);
+        u64 pw[8];
+        for (u32 a = 0; a < 8; a++) pw[a] = (u64)(((u128)1 << (8 * a)) % q);
+        for (u32 i = 0; i < 256; i++) {
+            u64 F[16][16], V[16][16];  // [k][j]
+            for (u32 j0 = 0; j0 < 16; j0++) {
+                u64 v[16] = {}, x[16] = {};
+                v[j0] = 1;
+                x[j0] = 1;
+                for (u32 m = 256; m <= 2048; m <<= 1) {
+                    const u32 tt = N / (2 * m), tj = tt / 16;
+                    for (u32 j = 0; j < 16; j++) {
+                        if (j & tj) continue;
+                        const u32 e = i * 256 + 16 * j;
+                        const u64 w = Tb[m + e / (2 * tt)];
+                        const u64 a = v[j], b = mulmod(v[j + tj], w, q);
+                        v[j] = a + b >= q ? a + b - q : a + b;
+                        v[j + tj] = a >= b ? a - b : a + q - b;
+                    }
+                }
+                for (u32 tt = 16; tt <= 128; tt <<= 1) {
+                    const u32 m = N / (2 * tt), tj = tt / 16;
+                    for (u32 j = 0; j < 16; j++) {
+                        if (j & tj) continue;
+                        const u32 e = i * 256 + 16 * j;
+                        const u64 w = TI[m + e / (2 * tt)];
+                        const u64 a = x[j], b = x[j + tj];
+                        x[j] = a + b >= q ? a + b - q : a + b;
+                        x[j + tj] = mulmod(a >= b ? a - b : a + q - b, w, q);
+                    }
+                }
+                for (u32 k = 0; k < 16; k++) {
+                    F[k][j0] = v[k];
+                    V[k][j0] = mulmod(x[k], scale, q);
+                }
+            }
+            for (u32 mat = 0; mat < 2; mat++) {
+                unsigned char* dst = tab.data() + ((size_t)t * 256 + i) * per_group + (size_t)mat * NM_FRAG * 16;
+                const u64(*A)[16] = mat ? V : F;
+                for (u32 mt = 0; mt < 4; mt++)
+                    for (u32 s = 0; s < 4; s++)
+                        for (u32 l = 0; l < 64; l++) {
+                            const u32 rr = l & 31, kh = l >> 5;
+                            const u32 dh = (rr >> 2) & 1, reg = (rr & 3) + 4 * (rr >> 3);
+                            const u32 k = 4 * mt + 2 * dh + (reg >> 3), bd = reg & 7;
+                            for (u32 e = 0; e < 16; e++) {
+                                const u32 j = 4 * s + 2 * kh + (e >> 3), a = e & 7;
+                                const u64 z = mulmod(pw[a], A[k][j], q) + DIGIT_BIAS;
+                                dst[(((size_t)mt * 4 + s) * 64 + l) * 16 + e] = (unsigned char)(((z >> (8 * bd)) & 0xFF) ^ 0x80);
+                            }
+                        }
+            }
+        }
+        BmRed& R = red[t];
+        R = BmRed{};
+        const unsigned L = msb64(q);
+        R.p = q;
+        R.np = 0 - q;
+        const u128 k = (((u128)1 << 80) + q - 1) / q;
+        const u128 bias = k * q;
+        R.bhi = (u64)(bias >> 32) - (1ull << 16);
+        R.blo = (u64)(bias & 0xFFFFFFFFull) + (1ull << 48);
+        R.p2 = 2 * q;
+        R.r60 = (1ull << L) - q;
+        R.r60p = (u64)(L - 32) | ((u64)((1u << (L - 32)) - 1) << 32);
+    };
+    {
+        unsigned nth = std::thread::hardware_concurrency();
+        if (nth < 1) nth = 1;
+        if (nth > T) nth = T;
+        if (nth > 16) nth = 16;
+        std::vector<std::thread> th;
+        for (unsigned w = 0; w < nth; w++)
+            th.emplace_back([&, w] {
+                for (u32 t = w; t < T; t += nth) build(t);
+            });
+        for (auto& x : th) x.join();
+    }
+    void* d = nullptr;
+    if (hipMalloc(&d, tab.size()) != hipSuccess) return false;
+    if (hipMemcpy(d, tab.data(), tab.size(), hipMemcpyHostToDevice) != hipSuccess) {
+        (void)hipFree(d);
+        return false;
+    }
+    p->d_nm = d;
+    p->nm_state = 1;
+    return true;
+}
+
+// the fused block pass: k_block_mma when the plan has its table, else k_block
+static void launch_fused_block(ofhe_plan_t p, const PlanArgs& a, const u64* src, u64* dst, const u64* b, u32 batch,
+                               hipStream_t s) {
+    if (!nm_ready(p)) {
+        launch_block<MODE_FUSED>(a, p->spq, src, dst, b, batch, s, p->split8);
+        return;
+    }
+    NmArgs Q;
+    Q.frag = reinterpret_cast<const i32x4*>(p->d_nm);
+    Q.red = reinterpret_cast<const BmRed*>(reinterpret_cast<const unsigned char*>(p->d_nm) +
+                                           (size_t)p->towers * 256 * 2 * NM_FRAG * 16);
+    const u32 b16 = (batch + NM_POLYS - 1) / NM_POLYS * NM_POLYS;
+    Q.chunk = b16 < OFHE_NM_CHUNK ? b16 : OFHE_NM_CHUNK;
+    Q.nchunks = (batch + Q.chunk - 1) / Q.chunk;
+    const u32 nwg = p->towers * 256 * Q.nchunks;
+    hipLaunchKernelGGL(k_block_mma, dim3(nwg), dim3(NM_THREADS), 0, s, a, Q, src, dst, b, batch, nwg);
+}
+
 int ofhe_hip_ntt_mul_intt(ofhe_plan_t p, const uint64_t* a_, const uint64_t* b, uint64_t* c,
                           uint32_t batch, void* stream) {
     int rc = check_common(p, batch);
@@ -641,7 +792,7 @@ int ofhe_hip_ntt_mul_intt(ofhe_plan_t p, const uint64_t* a_, const uint64_t* b, 
             hipStream_t sx = multi ? p->st[idx & 1] : s;
             const u64 off = (u64)b0 * words;
             launch_colpass(a, p->spq, p->split8, false, a_ + off, c + off, n, sx);
-            launch_block<MODE_FUSED>(a, p->spq, c + off, c + off, b + off, n, sx, p->split8);
+            launch_fused_block(p, a, c + off, c + off, b + off, n, sx);
             launch_colpass(a, p->spq, p->split8, true, c + off, c + off, n, sx);
         }
         if (multi) {
@@ -670,7 +821,7 @@ int ofhe_hip_ntt_mul_intt_stage(ofhe_plan_t p, int stage, const uint64_t* a_, co
     } else if (stage == 0) {
         launch_colpass(a, p->spq, p->split8, false, a_, c, batch, s);
     } else if (stage == 1) {
-        launch_block<MODE_FUSED>(a, p->spq, c, c, b, batch, s, p->split8);
+        launch_fused_block(p, a, c, c, b, batch, s);
     } else {
         launch_colpass(a, p->spq, p->split8, true, c, c, batch, s);
     }
