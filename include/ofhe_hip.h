@@ -272,6 +272,31 @@ int ofhe_hip_switch_modulus(ofhe_ctx_t ctx, const uint64_t* src, uint64_t* dst, 
 int ofhe_hip_automorphism(ofhe_plan_t plan, uint32_t k, int eval_form, const uint64_t* src, uint64_t* dst,
                           uint32_t batch, void* stream);
 
+/* ---- rescaling (callers of the path one tower down) ----
+ * x: [batch][towers][N] (x_stride words per batch entry) over plan towers
+ * 0..towers-1, canonical, all in evaluation form (eval_form != 0) or all in
+ * coefficient form; out: [batch][towers-1][N] (out_stride), may alias x.
+ * DCRTPolyImpl::DropLastElementAndScale (dcrtpoly-impl.h:746-768), CKKS / BFV
+ * rescaling with ql_ql_inv_modql_divql_modq[i] and ql_inv_modq[i], i <
+ * towers-1 (ckksrns-cryptoparameters.cpp:72-86):
+ *   out_i = x_i ql_inv_modq_i + [SwitchModulus(x_last) c_i]   (evaluation:
+ *   the last tower through the INTT, the switched term through the NTT);
+ *   coefficient form: out_i = NTT(x_i ql_inv_modq_i + SwitchModulus(x_last) c_i)
+ *   -- the reference switches these towers to evaluation form (lines 765-766).
+ * ql_inv_modq_i must be invertible mod q_i in evaluation form (it is
+ * q_last^-1 mod q_i). */
+int ofhe_hip_drop_last_and_scale(ofhe_plan_t plan, uint32_t towers, const uint64_t* x, uint64_t x_stride,
+                                 uint64_t* out, uint64_t out_stride, int eval_form,
+                                 const uint64_t* ql_ql_inv_modql_divql_modq, const uint64_t* ql_inv_modq,
+                                 uint32_t batch, void* stream);
+/* DCRTPolyImpl::ModReduce (dcrtpoly-impl.h:792-812), BGV modulus switching:
+ * delta = [x_last]_coefficient * neg_t_inv_modq mod q_last;
+ *   out_i = (x_i + [SwitchModulus(delta)] t) ql_inv_modq_i, the switched term
+ * through the NTT in evaluation form; the output keeps the input's form. */
+int ofhe_hip_mod_reduce(ofhe_plan_t plan, uint32_t towers, const uint64_t* x, uint64_t x_stride, uint64_t* out,
+                        uint64_t out_stride, int eval_form, uint64_t t, uint64_t neg_t_inv_modq,
+                        const uint64_t* ql_inv_modq, uint32_t batch, void* stream);
+
 /* ---- multi-GPU: evaluation-key broadcast over RCCL (xGMI) ----
  * the path shards by ciphertext batch with no exchange;
  * the one collective is the broadcast of the key-switching keys from a root

@@ -325,3 +325,58 @@ def crt_centered(x_coeff: np.ndarray, moduli):
         v %= M
         out.append(v - M if v > M // 2 else v)
     return out
+
+
+# ---------------------------------------------------------------------------
+# Rescaling: the callers that drop the last tower
+# ---------------------------------------------------------------------------
+def rescale_tables(q):
+    """QlQlInvModqlDivqlModq / qlInvModq for dropping the last of the towers q,
+    as ckksrns-cryptoparameters.cpp:65-86 (and bfvrns-cryptoparameters.cpp:
+    639-657) build them: Ql = prod(q[:-1]); result = (Ql^-1 mod ql) Ql / ql."""
+    ql, Ql = int(q[-1]), _prod(q[:-1])
+    result = (pow(Ql % ql, -1, ql) * Ql) // ql
+    return [result % int(qi) for qi in q[:-1]], [pow(ql, -1, int(qi)) for qi in q[:-1]]
+
+
+def drop_last_and_scale(x: np.ndarray, q, rq, eval_form: bool, c, a) -> np.ndarray:
+    """DCRTPolyImpl::DropLastElementAndScale, dcrtpoly-impl.h:746-768, on every
+    batch entry: x [B][L+1][N] -> [B][L][N]."""
+    L = len(q) - 1
+    x = np.ascontiguousarray(x, dtype=np.uint64)
+    last = x[:, L:L + 1]
+    if eval_form:  # lastPoly.SetFormat(Format::COEFFICIENT)
+        last = set_format(last, [q[L]], [rq[L]], False)
+    out = np.empty((x.shape[0], L, x.shape[2]), np.uint64)
+    for i in range(L):
+        qi = int(q[i])
+        tmp = switch_modulus(last[:, 0], int(q[L]), qi)[:, None]     # tmp.SwitchModulus
+        tmp = _scale(tmp, [c[i]], [qi])                             # tmp *= QlQlInvModqlDivqlModq[i]
+        if eval_form:
+            tmp = set_format(tmp, [qi], [rq[i]], True)              # tmp.SwitchFormat()
+        m = _scale(x[:, i:i + 1], [a[i]], [qi])                     # m_vectors[i] *= qlInvModq[i]
+        m = O.eltwise("add", m, tmp, [qi])                          # m_vectors[i] += tmp
+        if not eval_form:
+            m = set_format(m, [qi], [rq[i]], True)                  # m_vectors[i].SwitchFormat()
+        out[:, i:i + 1] = m
+    return out
+
+
+def mod_reduce(x: np.ndarray, q, rq, eval_form: bool, t: int, neg_t_inv_modq: int, a) -> np.ndarray:
+    """DCRTPolyImpl::ModReduce, dcrtpoly-impl.h:792-812: x [B][L+1][N] -> [B][L][N]."""
+    L = len(q) - 1
+    x = np.ascontiguousarray(x, dtype=np.uint64)
+    delta = x[:, L:L + 1]
+    if eval_form:  # delta.SetFormat(Format::COEFFICIENT)
+        delta = set_format(delta, [q[L]], [rq[L]], False)
+    delta = _scale(delta, [neg_t_inv_modq], [q[L]])                 # delta *= negtInvModq
+    out = np.empty((x.shape[0], L, x.shape[2]), np.uint64)
+    for i in range(L):
+        qi = int(q[i])
+        tmp = switch_modulus(delta[:, 0], int(q[L]), qi)[:, None]    # tmp.SwitchModulus
+        if eval_form:
+            tmp = set_format(tmp, [qi], [rq[i]], True)              # tmp.SwitchFormat()
+        tmp = _scale(tmp, [t], [qi])                                # tmp *= t
+        m = O.eltwise("add", np.ascontiguousarray(x[:, i:i + 1]), tmp, [qi])  # m_vectors[i] += tmp
+        out[:, i:i + 1] = _scale(m, [a[i]], [qi])                   # m_vectors[i] *= qlInvModq[i]
+    return out

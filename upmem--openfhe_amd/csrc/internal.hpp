@@ -116,6 +116,11 @@ struct ofhe_plan_s {
     std::mutex fork_mu;  // guards st / ev_* (plan_tune, the two-stream pipeline)
     // k_block_mma (ntt_mma.hpp): F_i / V_i fragments per (tower, group) and the
     // per-tower reduction constants, built on the first fused call
+    // rescaling scalar tables (keyswitch.hip: DropLastElementAndScale /
+    // ModReduce), uploaded once per distinct content into memory no launch
+    // has read yet, kept until destroy
+    std::mutex tab_mu;
+    std::map<std::vector<ofhe::u64>, ofhe::u64*> tabs;
     void* d_nm = nullptr;
     int nm_state = 0;  // 0 not built, 1 ready, -1 not applicable
     std::mutex nm_mu;

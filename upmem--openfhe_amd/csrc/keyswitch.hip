@@ -690,3 +690,140 @@ int ofhe_hip_automorphism(ofhe_plan_t p, uint32_t k, int eval_form, const uint64
                            dst, k, total, p->log_n, p->towers);
     return post_launch();
 }
+
+// ---------------------------------------------------------------------------
+// Rescaling on the device: DCRTPolyImpl::DropLastElementAndScale (CKKS / BFV,
+// dcrtpoly-impl.h:746-768) and DCRTPolyImpl::ModReduce (BGV, 792-812), the
+// callers that take the path's INTT -> SwitchModulus -> NTT steps one tower
+// down.  Evaluation form runs INTT(last tower) -> k_switch_scale<SW_SCALE> ->
+// the fused forward-subtract block pass, using
+//   x a + NTT(sw c) = (x - NTT(sw (-c a^-1))) a      (rescale, a = qlInvModq_i)
+//   (x + NTT(sw t)) a = (x - NTT(sw (-t))) a           (mod-reduce)
+// with the canonical residues of the reference's own order of operations.
+// ---------------------------------------------------------------------------
+static int plan_table(ofhe_plan_t p, const std::vector<u64>& words, const u64** out) {
+    std::lock_guard<std::mutex> lk(p->tab_mu);
+    auto it = p->tabs.find(words);
+    if (it != p->tabs.end()) {
+        *out = it->second;
+        return OFHE_OK;
+    }
+    u64* d = nullptr;
+    HIPCHK(hipMalloc(&d, words.size() * sizeof(u64)));
+    hipError_t e = hipMemcpy(d, words.data(), words.size() * sizeof(u64), hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+        (void)hipFree(d);
+        return fail(OFHE_ERR_HIP, std::string("rescale tables: ") + hipGetErrorString(e));
+    }
+    p->tabs.emplace(words, d);
+    *out = d;
+    return OFHE_OK;
+}
+
+static int rescale_check(ofhe_plan_t p, u32 towers, const u64* x, u64 xs, const u64* out, u64 os, u32 batch) {
+    if (!p || !p->ctx) return fail(OFHE_ERR_STATE, "plan is NULL or destroyed");
+    if (!x || !out || batch == 0) return fail(OFHE_ERR_ARG, "bad data argument");
+    // dcrtpoly-impl.h:720-723 (DropLastElement)
+    if (towers < 2) return fail(OFHE_ERR_ARG, "Removing last element of DCRTPoly object renders it invalid!");
+    if (towers > p->towers) return fail(OFHE_ERR_ARG, "towers exceeds the plan");
+    const u64 N = 1ull << p->log_n;
+    if (xs < towers * N || os < (towers - 1) * N) return fail(OFHE_ERR_ARG, "batch stride smaller than the towers");
+    return OFHE_OK;
+}
+
+// shared tail: sw[6 L] for k_switch_scale, sc[3 L] (q, a, a') for the
+// forward-subtract (evaluation form)
+static int rescale_run(ofhe_plan_t p, u32 towers, const u64* x, u64 xs, u64* out, u64 os, bool eval, int mode,
+                       const std::vector<u64>& sw, const std::vector<u64>& sc, u64 pre, u32 batch, hipStream_t s) {
+    HIPCHK(hipSetDevice(p->ctx->device));
+    const u32 L = towers - 1, log_n = p->log_n;
+    const u64 N = 1ull << log_n;
+    const u64 *dsw = nullptr, *dsc = nullptr;
+    RCCHK(plan_table(p, sw, &dsw));
+    if (eval) RCCHK(plan_table(p, sc, &dsc));
+    const u64 ql = p->q[L];
+    SwArgs A{};
+    A.tab = dsw;
+    A.ql = ql;
+    A.pre = pre % ql;
+    A.pre_p = shoup_pre(A.pre, ql);
+    if (A.pre == 1) A.pre_p = 0;
+    A.log_n = log_n;
+    A.towers = L;
+    const u32 bpr = (u32)((N + 255) / 256);
+    const u64 blocks = (u64)bpr * batch * L;
+    if (blocks >= (1ull << 31)) return fail(OFHE_ERR_ARG, "batch too large for one launch");
+    if (!eval) {
+        A.last = x + (u64)L * N;
+        A.lstride = xs;
+        A.x = x;
+        A.xstride = xs;
+        A.y = out;
+        A.ystride = os;
+        if (mode == SW_AXPY)
+            hipLaunchKernelGGL(k_switch_scale<SW_AXPY>, dim3((u32)blocks), dim3(256), 0, s, A, bpr);
+        else
+            hipLaunchKernelGGL(k_switch_scale<SW_XPYA>, dim3((u32)blocks), dim3(256), 0, s, A, bpr);
+        RCCHK(post_launch());
+        // DropLastElementAndScale switches the coefficient-form towers to
+        // evaluation form (dcrtpoly-impl.h:765-766); ModReduce does not
+        if (mode == SW_AXPY) return plan_ntt_range(p, false, 0, L, out, out, os, os, batch, s);
+        return OFHE_OK;
+    }
+    Scratch sl, sy;
+    RCCHK(sl.alloc((size_t)batch * N * 8, s));
+    RCCHK(sy.alloc((size_t)batch * L * N * 8, s));
+    RCCHK(plan_ntt_range(p, true, L, 1, x + (u64)L * N, sl.w(), xs, N, batch, s));
+    A.last = sl.w();
+    A.lstride = N;
+    A.y = sy.w();
+    A.ystride = (u64)L * N;
+    hipLaunchKernelGGL(k_switch_scale<SW_SCALE>, dim3((u32)blocks), dim3(256), 0, s, A, bpr);
+    RCCHK(post_launch());
+    const u64 ys = (u64)L * N;
+    if (log_n >= 12) return plan_ntt_fwd_sub(p, 0, L, sy.w(), ys, x, xs, out, os, dsc, batch, s);
+    RCCHK(plan_ntt_range(p, false, 0, L, sy.w(), sy.w(), ys, ys, batch, s));
+    return sub_scale(reinterpret_cast<const TowerScalar*>(dsc), x, sy.w(), out, xs, ys, os, batch, L, log_n, s);
+}
+
+int ofhe_hip_drop_last_and_scale(ofhe_plan_t p, uint32_t towers, const uint64_t* x, uint64_t x_stride,
+                                 uint64_t* out, uint64_t out_stride, int eval_form,
+                                 const uint64_t* ql_ql_inv_modql_divql_modq, const uint64_t* ql_inv_modq,
+                                 uint32_t batch, void* stream) {
+    RCCHK(rescale_check(p, towers, x, x_stride, out, out_stride, batch));
+    if (!ql_ql_inv_modql_divql_modq || !ql_inv_modq) return fail(OFHE_ERR_ARG, "NULL constants");
+    const u32 L = towers - 1;
+    std::vector<u64> sw(6 * (size_t)L, 0), sc(3 * (size_t)L, 0);
+    for (u32 i = 0; i < L; i++) {
+        const u64 q = p->q[i], c = ql_ql_inv_modql_divql_modq[i] % q, a = ql_inv_modq[i] % q;
+        if (eval_form) {
+            if (a == 0) return fail(OFHE_ERR_ARG, "ql_inv_modq[" + std::to_string(i) + "] is not invertible mod q_i");
+            const u64 w = (q - mulmod(c, invmod(a, q), q)) % q;
+            const TowerScalar W = scalar_of(q, w), S = scalar_of(q, a);
+            sw[6 * i] = q, sw[6 * i + 1] = W.s, sw[6 * i + 2] = W.sp;
+            sc[3 * i] = q, sc[3 * i + 1] = S.s, sc[3 * i + 2] = S.sp;
+        } else {
+            const TowerScalar W = scalar_of(q, c), S = scalar_of(q, a);
+            sw[6 * i] = q, sw[6 * i + 1] = W.s, sw[6 * i + 2] = W.sp, sw[6 * i + 3] = S.s, sw[6 * i + 4] = S.sp;
+        }
+    }
+    return rescale_run(p, towers, x, x_stride, out, out_stride, eval_form != 0, SW_AXPY, sw, sc, 1, batch,
+                       pick(stream));
+}
+
+int ofhe_hip_mod_reduce(ofhe_plan_t p, uint32_t towers, const uint64_t* x, uint64_t x_stride, uint64_t* out,
+                        uint64_t out_stride, int eval_form, uint64_t t, uint64_t neg_t_inv_modq,
+                        const uint64_t* ql_inv_modq, uint32_t batch, void* stream) {
+    RCCHK(rescale_check(p, towers, x, x_stride, out, out_stride, batch));
+    if (!ql_inv_modq) return fail(OFHE_ERR_ARG, "NULL constants");
+    const u32 L = towers - 1;
+    std::vector<u64> sw(6 * (size_t)L, 0), sc(3 * (size_t)L, 0);
+    for (u32 i = 0; i < L; i++) {
+        const u64 q = p->q[i], tq = t % q, a = ql_inv_modq[i] % q;
+        const TowerScalar W = scalar_of(q, eval_form ? (q - tq) % q : tq), S = scalar_of(q, a);
+        sw[6 * i] = q, sw[6 * i + 1] = W.s, sw[6 * i + 2] = W.sp, sw[6 * i + 3] = S.s, sw[6 * i + 4] = S.sp;
+        sc[3 * i] = q, sc[3 * i + 1] = S.s, sc[3 * i + 2] = S.sp;
+    }
+    return rescale_run(p, towers, x, x_stride, out, out_stride, eval_form != 0, SW_XPYA, sw, sc, neg_t_inv_modq,
+                       batch, pick(stream));
+}

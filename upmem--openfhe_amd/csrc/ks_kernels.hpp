@@ -246,6 +246,55 @@ __global__ __launch_bounds__(256) void k_switch_modulus(const u64* src, u64* dst
     }
 }
 
+// Rescaling callers of SwitchModulus (dcrtpoly-impl.h:746-768 and 792-812):
+// the dropped tower's coefficients v (canonical mod ql), optionally scaled
+// first by pre (ModReduce's delta *= negtInvModq), are lifted into every
+// remaining q_i and combined per tower with the scalars of tab[i] =
+// (q_i, w_i, w_i', a_i, a_i', 0):
+//   SW_SCALE  y = sw(v) w                   (evaluation form; the NTT and the
+//                                            x a / (x - .) a step follow in
+//                                            the fused forward-subtract pass)
+//   SW_AXPY   y = x a + sw(v) w             (DropLastElementAndScale, coefficient form)
+//   SW_XPYA   y = (x + sw(v) w) a           (ModReduce, coefficient form)
+// one thread per (batch entry, tower, coefficient); canonical outputs.
+enum { SW_SCALE = 0, SW_AXPY = 1, SW_XPYA = 2 };
+struct SwArgs {
+    const u64* last;  // [batch] rows of N (stride lstride)
+    u64 lstride;
+    const u64* x;     // [batch][towers][N] (stride xstride), SW_AXPY / SW_XPYA
+    u64 xstride;
+    u64* y;           // [batch][towers][N] (stride ystride)
+    u64 ystride;
+    const u64* tab;   // [towers][6]
+    u64 ql, pre, pre_p;  // pre: scalar on v mod ql first (1: none)
+    u32 log_n, towers;
+};
+// NativeVectorT::SwitchModulus (mubintvecnat.cpp:111-136) of one value
+__device__ __forceinline__ u64 switch_mod1(u64 v, u64 om, u64 nm) {
+    if (v > (om >> 1)) v += nm > om ? nm - om : nm - (om % nm);
+    if (nm <= om && v >= nm) v = om <= 2 * nm ? csub(csub(v, nm), nm) : v % nm;  // v < om + nm
+    return v;
+}
+template <int MODE>
+__global__ __launch_bounds__(256) void k_switch_scale(SwArgs A, u32 bpr) {
+    const u32 row = blockIdx.x / bpr, b = row / A.towers, t = row % A.towers;  // bpr blocks per row
+    const u64 N = 1ull << A.log_n;
+    const u64 j = (u64)(blockIdx.x % bpr) * blockDim.x + threadIdx.x;
+    if (j >= N) return;
+    const u64* T = A.tab + 6 * (u64)t;
+    const u64 q = T[0], w = T[1], wp = T[2], a = T[3], ap = T[4];
+    u64 v = A.last[b * A.lstride + j];
+    if (A.pre != 1) v = shoup_canon(v, A.pre, A.pre_p, A.ql);
+    const u64 sv = shoup_canon(switch_mod1(v, A.ql, q), w, wp, q);
+    u64 r = sv;
+    if (MODE == SW_AXPY) {
+        r = csub(shoup_canon(A.x[b * A.xstride + (u64)t * N + j], a, ap, q) + sv, q);
+    } else if (MODE == SW_XPYA) {
+        r = shoup_canon(csub(A.x[b * A.xstride + (u64)t * N + j] + sv, q), a, ap, q);
+    }
+    A.y[b * A.ystride + (u64)t * N + j] = r;
+}
+
 // PolyImpl::AutomorphismTransform(k) (poly-impl.h:338-364).  One thread per
 // index j of one (batch, tower) row:
 //   evaluation form:  dst[rev(j)] = src[rev(((k (2j+1)) >> 1) mod n)]

@@ -376,6 +376,7 @@ int ofhe_hip_plan_destroy(ofhe_plan_t p) {
     (void)hipFree(p->d_twist);
     (void)hipFree(p->d_twist_r);
     (void)hipFree(p->d_nm);
+    for (auto& kv : p->tabs) (void)hipFree(kv.second);
     delete p;
     return OFHE_OK;
 }

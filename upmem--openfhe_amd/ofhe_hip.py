@@ -103,6 +103,10 @@ _SIGS = {
     "ofhe_hip_switch_modulus": (ctypes.c_int, [_vp, _vp, _vp, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64,
                                                _vp]),
     "ofhe_hip_automorphism": (ctypes.c_int, [_vp, ctypes.c_uint32, ctypes.c_int, _vp, _vp, ctypes.c_uint32, _vp]),
+    "ofhe_hip_drop_last_and_scale": (ctypes.c_int, [_vp, ctypes.c_uint32, _vp, ctypes.c_uint64, _vp, ctypes.c_uint64,
+                                                    ctypes.c_int, _vp, _vp, ctypes.c_uint32, _vp]),
+    "ofhe_hip_mod_reduce": (ctypes.c_int, [_vp, ctypes.c_uint32, _vp, ctypes.c_uint64, _vp, ctypes.c_uint64,
+                                           ctypes.c_int, ctypes.c_uint64, ctypes.c_uint64, _vp, ctypes.c_uint32, _vp]),
     "ofhe_hip_comm_unique_id": (ctypes.c_int, [_vp]),
     "ofhe_hip_comm_init": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int, _vp, ctypes.POINTER(_vp)]),
     "ofhe_hip_comm_destroy": (ctypes.c_int, [_vp]),
@@ -333,6 +337,27 @@ class NTTPlan:
         """PolyImpl::AutomorphismTransform(k) on every (batch, tower); dst must not alias src."""
         _check(lib().ofhe_hip_automorphism(self.handle, int(k), 1 if eval_form else 0, _vp(src), _vp(dst),
                                            int(batch), _vp(stream or None)))
+
+    # --- rescaling (DCRTPolyImpl::DropLastElementAndScale / ModReduce) ---
+    def drop_last_and_scale(self, towers: int, x: int, x_stride: int, out: int, out_stride: int, eval_form: bool,
+                            ql_ql_inv_modql_divql_modq, ql_inv_modq, batch: int = 1, stream: int = 0) -> None:
+        """dcrtpoly-impl.h:746-768 on [batch][towers] -> [batch][towers - 1] (out may alias x)."""
+        c, a = list(ql_ql_inv_modql_divql_modq), list(ql_inv_modq)
+        if len(c) < towers - 1 or len(a) < towers - 1:
+            raise MathError("need towers - 1 constants")
+        _check(lib().ofhe_hip_drop_last_and_scale(self.handle, int(towers), _vp(x), int(x_stride), _vp(out),
+                                                  int(out_stride), 1 if eval_form else 0, _arr(c), _arr(a), int(batch),
+                                                  _vp(stream or None)))
+
+    def mod_reduce(self, towers: int, x: int, x_stride: int, out: int, out_stride: int, eval_form: bool, t: int,
+                   neg_t_inv_modq: int, ql_inv_modq, batch: int = 1, stream: int = 0) -> None:
+        """dcrtpoly-impl.h:792-812 on [batch][towers] -> [batch][towers - 1] (out may alias x)."""
+        a = list(ql_inv_modq)
+        if len(a) < towers - 1:
+            raise MathError("need towers - 1 constants")
+        _check(lib().ofhe_hip_mod_reduce(self.handle, int(towers), _vp(x), int(x_stride), _vp(out), int(out_stride),
+                                         1 if eval_form else 0, int(t), int(neg_t_inv_modq), _arr(a), int(batch),
+                                         _vp(stream or None)))
 
     # --- the metric pipeline ---
     def ntt_mul_intt(self, a: int, b: int, c: int, batch: int = 1, stream: int = 0) -> None:
