@@ -359,6 +359,75 @@ int main() {
         EXPECT_THROW(ks.KeySwitchCore(C, SnQP, KA), math_error, "wrong key shape");
     });
     // AutomorphismTransform: sigma_k then sigma_k^-1 is the identity, both forms
+    // DropLastElementAndScale / ModReduce (dcrtpoly-impl.h:746-812) with the
+    // reference's constants (ckksrns-cryptoparameters.cpp:72-86; there
+    // QlQlInvModqlDivqlModq_i = ((Ql^-1 mod ql) Ql - 1) / ql = -ql^-1 mod q_i):
+    // X = ql Y + e with |e| < ql / 2 rescales to Y; X = ql Y + t e with small e
+    // mod-reduces to Y -- from either form.
+    TEST("DCRTPolyHip.rescale_and_mod_reduce", [] {
+        const uint32_t m = 1u << 12, n = m / 2, batch = 2, T = 4;
+        std::vector<uint64_t> q;
+        uint64_t x = first_prime(60, m);
+        for (uint32_t t = 0; t < T; t++) q.push_back(x = previous_prime(x, m));
+        const uint64_t ql = q[T - 1], t_ = 65537;
+        std::vector<uint64_t> a, c;
+        for (uint32_t i = 0; i + 1 < T; i++) {
+            a.push_back(powmod(ql % q[i], q[i] - 2, q[i]));
+            c.push_back(q[i] - a.back());
+        }
+        const uint64_t negtinv = ql - powmod(t_ % ql, ql - 2, ql);
+        std::mt19937_64 rng(9);
+        std::vector<int64_t> Y((size_t)batch * n), E((size_t)batch * n), Et((size_t)batch * n);
+        for (size_t j = 0; j < Y.size(); j++) {
+            Y[j] = (int64_t)(rng() % (1u << 20)) - (1 << 19);
+            E[j] = (int64_t)(rng() % (ql - 1)) - (int64_t)(ql / 2 - 1);   // |e| < ql / 2
+            Et[j] = (int64_t)(rng() % (1u << 30)) - (1 << 29);           // t e small
+        }
+        auto residues = [&](const std::vector<int64_t>& e, uint64_t scale_e, const std::vector<uint64_t>& mods) {
+            std::vector<uint64_t> v((size_t)batch * mods.size() * n);
+            for (uint32_t b = 0; b < batch; b++)
+                for (size_t t = 0; t < mods.size(); t++)
+                    for (uint32_t j = 0; j < n; j++) {
+                        const uint64_t mq = mods[t];
+                        const __int128 X = (__int128)ql * Y[b * n + j] + (__int128)scale_e * e[b * n + j];
+                        __int128 r = X % (__int128)mq;
+                        if (r < 0) r += mq;
+                        v[((size_t)b * mods.size() + t) * n + j] = (uint64_t)r;
+                    }
+            return v;
+        };
+        std::vector<uint64_t> ql_low(q.begin(), q.end() - 1);
+        auto PQ = params(m, q), PL = params(m, ql_low);
+        // expected: Y in coefficient form over the lower chain
+        std::vector<uint64_t> yres((size_t)batch * (T - 1) * n);
+        for (uint32_t b = 0; b < batch; b++)
+            for (uint32_t t = 0; t + 1 < T; t++)
+                for (uint32_t j = 0; j < n; j++) {
+                    const int64_t yv1 = Y[b * n + j];
+                    yres[((size_t)b * (T - 1) + t) * n + j] = yv1 < 0 ? q[t] - (uint64_t)(-yv1) : (uint64_t)yv1;
+                }
+        DCRTPolyHip want(PL, Format::COEFFICIENT, batch);
+        want.SetValues(yres, Format::COEFFICIENT);
+        for (int ev = 0; ev < 2; ev++) {
+            DCRTPolyHip X(PQ, Format::COEFFICIENT, batch);
+            X.SetValues(residues(E, 1, q), Format::COEFFICIENT);
+            if (ev) X.SwitchFormat();
+            X.DropLastElementAndScale(c, a);
+            EXPECT_EQ(X.GetFormat() == Format::EVALUATION, true, "rescale output in evaluation form");
+            EXPECT_EQ(X.GetParams()->Towers(), (size_t)(T - 1), "one tower dropped");
+            X.SwitchFormat();
+            EXPECT_EQ(X, want, ev ? "rescale (evaluation input)" : "rescale (coefficient input)");
+            DCRTPolyHip Z(PQ, Format::COEFFICIENT, batch);
+            Z.SetValues(residues(Et, t_, q), Format::COEFFICIENT);
+            if (ev) Z.SwitchFormat();
+            Z.ModReduce(t_, negtinv, a);
+            EXPECT_EQ(Z.GetFormat() == (ev ? Format::EVALUATION : Format::COEFFICIENT), true, "mod-reduce keeps the form");
+            if (ev) Z.SwitchFormat();
+            EXPECT_EQ(Z, want, ev ? "mod-reduce (evaluation input)" : "mod-reduce (coefficient input)");
+        }
+        DCRTPolyHip one(params(m, std::vector<uint64_t>{q[0]}), Format::EVALUATION, 1);
+        EXPECT_THROW(one.DropLastElementAndScale(c, a), math_error, "DropLastElement of one tower");
+    });
     TEST("DCRTPolyHip.automorphism_inverse", [] {
         const uint32_t m = 1u << 12, n = m / 2;
         auto P = params(m, {first_prime(50, m), next_prime(first_prime(50, m), m)});

@@ -362,6 +362,36 @@ public:
         check(ofhe_hip_modmul_vv(p_->plan(), data(), rhs.data(), r.data(), batch_, nullptr), "Times");
         return r;
     }
+    // DropLastElementAndScale (dcrtpoly-impl.h:746-768; CKKS / BFV rescaling):
+    // one tower fewer, on the params of the shorter chain.  The reference keeps
+    // m_format while its coefficient-form towers come back in evaluation form
+    // (lines 765-766); here the format tag follows the data (EVALUATION).
+    void DropLastElementAndScale(const std::vector<uint64_t>& QlQlInvModqlDivqlModq,
+                                 const std::vector<uint64_t>& qlInvModq) {
+        const size_t T = p_->Towers(), n = p_->GetRingDimension();
+        if (QlQlInvModqlDivqlModq.size() + 1 < T || qlInvModq.size() + 1 < T)
+            throw math_error("DropLastElementAndScale: one constant per remaining tower required");
+        auto lp = lower_params();
+        DCRTPolyHip r(lp, Format::EVALUATION, batch_, Uninit{});
+        check(ofhe_hip_drop_last_and_scale(p_->plan(), (uint32_t)T, data(), T * n, r.data(), (T - 1) * n,
+                                           f_ == Format::EVALUATION, QlQlInvModqlDivqlModq.data(), qlInvModq.data(),
+                                           batch_, nullptr),
+              "DropLastElementAndScale");
+        *this = std::move(r);
+    }
+    // ModReduce (dcrtpoly-impl.h:792-812; BGV modulus switching): one tower
+    // fewer, format unchanged
+    void ModReduce(uint64_t t, uint64_t negtInvModq, const std::vector<uint64_t>& qlInvModq) {
+        const size_t T = p_->Towers(), n = p_->GetRingDimension();
+        if (qlInvModq.size() + 1 < T) throw math_error("ModReduce: one constant per remaining tower required");
+        auto lp = lower_params();
+        DCRTPolyHip r(lp, f_, batch_, Uninit{});
+        check(ofhe_hip_mod_reduce(p_->plan(), (uint32_t)T, data(), T * n, r.data(), (T - 1) * n,
+                                  f_ == Format::EVALUATION, t, negtInvModq, qlInvModq.data(), batch_, nullptr),
+              "ModReduce");
+        *this = std::move(r);
+    }
+
     // Times(const std::vector<NativeInteger>&): one scalar per tower (Shoup)
     DCRTPolyHip Times(const std::vector<uint64_t>& scalars) const {
         if (scalars.size() != p_->Towers()) throw math_error("Times: one scalar per tower required");
@@ -436,6 +466,15 @@ public:
     }
 
 private:
+    // DropLastElement (dcrtpoly-impl.h:719-728): the params of the chain
+    // without its last tower (a cached plan of that basis)
+    std::shared_ptr<DCRTParams> lower_params() const {
+        if (p_->Towers() < 2) throw math_error("Removing last element of DCRTPoly object renders it invalid!");
+        std::vector<uint64_t> q(p_->Moduli().begin(), p_->Moduli().end() - 1);
+        std::vector<uint64_t> r(p_->Roots().begin(), p_->Roots().end() - 1);
+        return std::make_shared<DCRTParams>(p_->GetCyclotomicOrder(), q, r, p_->manager()->device());
+    }
+
     void check_compat(const DCRTPolyHip& rhs, const char* op, bool eval_only, bool same_format = true) const {
         if (p_->GetRingDimension() != rhs.p_->GetRingDimension())
             throw math_error(std::string(op) + ": RingDimension missmatch");
