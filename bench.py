@@ -371,6 +371,7 @@ def bench_pipeline(args):
     if not args.no_extras:
         extras["configs3"] = bench_configs3(args, ctx, world, rank, dev)
         extras["keyswitch"] = bench_keyswitch(args, ctx, world, rank, dev, steps=args.ks_steps, warmup=2)
+        extras["rescale"] = bench_rescale(args, ctx, world, rank, dev, steps=args.ks_steps, warmup=2)
         if rank == 0 and world == 1:
             extras["pcie_inclusive"] = (pcie_inclusive(plan, args.pcie_batch, args.pcie_chunks, dev)
                                         if args.pcie_chunks > 0 else None)
@@ -408,6 +409,7 @@ def bench_pipeline(args):
             "evalkey_broadcast": bcast,
             "configs3": extras.get("configs3"),
             "keyswitch": extras.get("keyswitch"),
+            "rescale": extras.get("rescale"),
             "configs0": extras.get("configs0"),
             "pcie_inclusive": extras.get("pcie_inclusive"),
             "build_id": build_id(),
@@ -514,6 +516,51 @@ def bench_configs3(args, ctx, world, rank, dev):
             "value": total * steps / elapsed, "unit": "coeffs/s", "scaling": "strong", "steps": steps,
             "ms_per_step": elapsed / steps * 1e3, "hbm_frac_per_gpu": total / world * 24 / (elapsed / steps) / 8e12,
             "towers_per_rank": T}
+
+
+# ---------------------------------------------------------------------------
+# CKKS rescaling (DCRTPolyImpl::DropLastElementAndScale, evaluation form) on
+# configs[4]'s ring: 48 -> 47 towers at N = 2^17, a batch of ciphertext
+# polynomials per GPU (batch-sharded)
+# ---------------------------------------------------------------------------
+def bench_rescale(args, ctx, world, rank, dev, steps, warmup):
+    import torch
+    import torch.distributed as dist
+
+    import ofhe_hip as H
+    import shard
+
+    log_n, T = 17, 48
+    n = 1 << log_n
+    q, rq = moduli_chain(log_n, T)
+    B = args.ks_batch
+    ql = q[-1]
+    a = [pow(ql, -1, qi) for qi in q[:-1]]  # qlInvModq
+    c = [qi - ai for qi, ai in zip(q[:-1], a)]  # QlQlInvModqlDivqlModq = -ql^-1 mod q_i
+    plan = H.NTTPlan(ctx, log_n, q, rq)
+    stream = torch.cuda.current_stream(dev)
+    sptr = stream.cuda_stream
+    b0, _ = shard.shard_batch(B * world, rank, world)
+    x = torch.empty((B, T, n), dtype=torch.int64, device=dev)
+    plan.fill_uniform(x.data_ptr(), B, 8, b0, sptr)
+    out = torch.empty((B, T - 1, n), dtype=torch.int64, device=dev)
+
+    def step():
+        plan.drop_last_and_scale(T, x.data_ptr(), T * n, out.data_ptr(), (T - 1) * n, True, c, a, B, sptr)
+
+    elapsed, ev_ms = _timed(step, steps, warmup, stream, world, dev)
+    del x, out
+    plan.close()
+    torch.cuda.empty_cache()
+    if world > 1:
+        dist.barrier()
+    per = elapsed / steps
+    return {"workload": f"DropLastElementAndScale (CKKS rescale), N=2^17, {T} -> {T - 1} towers, evaluation form, "
+                        f"batch {B} per GPU",
+            "value": B * world / per, "unit": "rescales/s", "scaling": "weak", "steps": steps,
+            "ms_per_step": per * 1e3, "ms_per_step_events": ev_ms,
+            "alg_hbm_gbs": B * (2 * T - 1) * n * 8 / per / 1e9,
+            "note": "algorithmic bytes: read T towers, write T - 1 (8 B per word)"}
 
 
 # ---------------------------------------------------------------------------

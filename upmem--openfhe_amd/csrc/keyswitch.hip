@@ -728,6 +728,8 @@ static int rescale_check(ofhe_plan_t p, u32 towers, const u64* x, u64 xs, const 
     if (towers > p->towers) return fail(OFHE_ERR_ARG, "towers exceeds the plan");
     const u64 N = 1ull << p->log_n;
     if (xs < towers * N || os < (towers - 1) * N) return fail(OFHE_ERR_ARG, "batch stride smaller than the towers");
+    if (((xs | os) & 1) || (((uintptr_t)x | (uintptr_t)out) & 15))
+        return fail(OFHE_ERR_ARG, "strides must be even and buffers 16-byte aligned");
     return OFHE_OK;
 }
 
@@ -750,7 +752,7 @@ static int rescale_run(ofhe_plan_t p, u32 towers, const u64* x, u64 xs, u64* out
     if (A.pre == 1) A.pre_p = 0;
     A.log_n = log_n;
     A.towers = L;
-    const u32 bpr = (u32)((N + 255) / 256);
+    const u32 bpr = (u32)((N / 2 + 255) / 256);  // two coefficients per thread
     const u64 blocks = (u64)bpr * batch * L;
     if (blocks >= (1ull << 31)) return fail(OFHE_ERR_ARG, "batch too large for one launch");
     if (!eval) {

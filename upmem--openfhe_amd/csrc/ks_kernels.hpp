@@ -275,24 +275,33 @@ __device__ __forceinline__ u64 switch_mod1(u64 v, u64 om, u64 nm) {
     if (nm <= om && v >= nm) v = om <= 2 * nm ? csub(csub(v, nm), nm) : v % nm;  // v < om + nm
     return v;
 }
+// two coefficients per thread (16-byte accesses); w = 1 (DropLastElementAndScale
+// with the reference's constants, where QlQlInvModqlDivqlModq = -qlInvModq)
+// skips the multiply
 template <int MODE>
 __global__ __launch_bounds__(256) void k_switch_scale(SwArgs A, u32 bpr) {
     const u32 row = blockIdx.x / bpr, b = row / A.towers, t = row % A.towers;  // bpr blocks per row
     const u64 N = 1ull << A.log_n;
-    const u64 j = (u64)(blockIdx.x % bpr) * blockDim.x + threadIdx.x;
+    const u64 j = 2 * ((u64)(blockIdx.x % bpr) * blockDim.x + threadIdx.x);
     if (j >= N) return;
     const u64* T = A.tab + 6 * (u64)t;
     const u64 q = T[0], w = T[1], wp = T[2], a = T[3], ap = T[4];
-    u64 v = A.last[b * A.lstride + j];
-    if (A.pre != 1) v = shoup_canon(v, A.pre, A.pre_p, A.ql);
-    const u64 sv = shoup_canon(switch_mod1(v, A.ql, q), w, wp, q);
-    u64 r = sv;
-    if (MODE == SW_AXPY) {
-        r = csub(shoup_canon(A.x[b * A.xstride + (u64)t * N + j], a, ap, q) + sv, q);
-    } else if (MODE == SW_XPYA) {
-        r = shoup_canon(csub(A.x[b * A.xstride + (u64)t * N + j] + sv, q), a, ap, q);
+    const ulonglong2 lv = *reinterpret_cast<const ulonglong2*>(A.last + b * A.lstride + j);
+    u64 r[2] = {lv.x, lv.y};
+    ulonglong2 xv = make_ulonglong2(0, 0);
+    if (MODE != SW_SCALE) xv = *reinterpret_cast<const ulonglong2*>(A.x + b * A.xstride + (u64)t * N + j);
+    const u64 xs[2] = {xv.x, xv.y};
+#pragma unroll
+    for (int k = 0; k < 2; k++) {
+        u64 v = r[k];
+        if (A.pre != 1) v = shoup_canon(v, A.pre, A.pre_p, A.ql);
+        v = switch_mod1(v, A.ql, q);
+        if (w != 1) v = shoup_canon(v, w, wp, q);
+        if (MODE == SW_AXPY) v = csub(shoup_canon(xs[k], a, ap, q) + v, q);
+        if (MODE == SW_XPYA) v = shoup_canon(csub(xs[k] + v, q), a, ap, q);
+        r[k] = v;
     }
-    A.y[b * A.ystride + (u64)t * N + j] = r;
+    st2_s(A.y + b * A.ystride + (u64)t * N + j, u64x2{r[0], r[1]});
 }
 
 // PolyImpl::AutomorphismTransform(k) (poly-impl.h:338-364).  One thread per

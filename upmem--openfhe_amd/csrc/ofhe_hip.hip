@@ -52,6 +52,17 @@ int ofhe_hip_init(int device, ofhe_ctx_t* ctx) {
     HIPCHK(hipGetDeviceCount(&n));
     if (device < 0 || device >= n) return fail(OFHE_ERR_ARG, "device index out of range");
     HIPCHK(hipSetDevice(device));
+    // Stream-ordered scratch (hipMallocAsync: ApproxModDown, key switching,
+    // rescaling) stays in the device's default pool across synchronisations
+    // instead of going back to the driver at every sync and being mapped again
+    // by the next call (a rescale timed call by call: 0.79 -> see DESIGN.md).
+    {
+        hipMemPool_t pool = nullptr;
+        if (hipDeviceGetDefaultMemPool(&pool, device) == hipSuccess && pool) {
+            uint64_t keep = UINT64_MAX;
+            (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep);
+        }
+    }
     ofhe_ctx_s* c = new (std::nothrow) ofhe_ctx_s();
     if (!c) return fail(OFHE_ERR_NOMEM, "context allocation failed");
     c->device = device;
