@@ -13,6 +13,9 @@ import torch  # noqa: E402
 import bench  # noqa: E402
 import ofhe_hip as H  # noqa: E402
 
+if os.environ.get("RS_LIB"):  # an A/B variant build (make variant)
+    H.LIB_PATH = os.path.join(ROOT, os.environ["RS_LIB"])
+
 log_n, T, B = 17, 48, int(os.environ.get("RS_BATCH", "8"))
 ev = os.environ.get("RS_EVAL", "1") == "1"
 n = 1 << log_n
@@ -35,5 +38,5 @@ for i in range(int(os.environ.get("RS_REPS", "20"))):
     e1.synchronize()
     ts.append(e0.elapsed_time(e1))
 med = statistics.median(ts[2:])
-print(f"rescale N=2^17 {T}->{T - 1} towers batch {B} eval={ev}: {med:.3f} ms, "
+print(f"[{os.path.basename(H.LIB_PATH)}] rescale N=2^17 {T}->{T - 1} towers batch {B} eval={ev}: {med:.3f} ms, "
       f"{B * (2 * T - 1) * n * 8 / med / 1e6:.0f} GB/s algorithmic")

@@ -37,6 +37,13 @@ __device__ __forceinline__ u64 mad32(u32 a, u32 b, u64 c) { return (u64)a * (u64
 
 __device__ __forceinline__ u64 csub(u64 x, u64 m) { return x >= m ? x - m : x; }
 
+// NativeVectorT::SwitchModulus (mubintvecnat.cpp:111-136) of one value
+__device__ __forceinline__ u64 switch_mod1(u64 v, u64 om, u64 nm) {
+    if (v > (om >> 1)) v += nm > om ? nm - om : nm - (om % nm);
+    if (nm <= om && v >= nm) v = om <= 2 * nm ? csub(csub(v, nm), nm) : v % nm;  // v < om + nm
+    return v;
+}
+
 // csub for a wave-uniform m (held in SGPRs: the NTT kernels' per-tower
 // moduli).  The compiler emits v_cmp_u64 + 2 cndmask + sub/subb (5 VALU ops)
 // for csub; this selects on the borrow of the subtraction itself (sub_co,

@@ -701,6 +701,9 @@ int ofhe_hip_automorphism(ofhe_plan_t p, uint32_t k, int eval_form, const uint64
 //   (x + NTT(sw t)) a = (x - NTT(sw (-t))) a           (mod-reduce)
 // with the canonical residues of the reference's own order of operations.
 // ---------------------------------------------------------------------------
+#ifndef OFHE_RESCALE_FUSE
+#define OFHE_RESCALE_FUSE 1  // 0: k_switch_scale then the column pass (A/B)
+#endif
 static int plan_table(ofhe_plan_t p, const std::vector<u64>& words, const u64** out) {
     std::lock_guard<std::mutex> lk(p->tab_mu);
     auto it = p->tabs.find(words);
@@ -776,13 +779,19 @@ static int rescale_run(ofhe_plan_t p, u32 towers, const u64* x, u64 xs, u64* out
     RCCHK(sl.alloc((size_t)batch * N * 8, s));
     RCCHK(sy.alloc((size_t)batch * L * N * 8, s));
     RCCHK(plan_ntt_range(p, true, L, 1, x + (u64)L * N, sl.w(), xs, N, batch, s));
+    const u64 ys = (u64)L * N;
+    if (log_n > 12 && !p->split8 && A.pre == 1 && OFHE_RESCALE_FUSE) {
+        // the lift happens in the column pass's loads (k_cols<.., SWS>): the
+        // switched towers are never written to HBM before their transform
+        RCCHK(plan_cols_switch(p, 0, L, sl.w(), N, ql, dsw, sy.w(), ys, batch, s));
+        return plan_ntt_fwd_sub(p, 0, L, sy.w(), ys, x, xs, out, os, dsc, batch, s, 2);
+    }
     A.last = sl.w();
     A.lstride = N;
     A.y = sy.w();
-    A.ystride = (u64)L * N;
+    A.ystride = ys;
     hipLaunchKernelGGL(k_switch_scale<SW_SCALE>, dim3((u32)blocks), dim3(256), 0, s, A, bpr);
     RCCHK(post_launch());
-    const u64 ys = (u64)L * N;
     if (log_n >= 12) return plan_ntt_fwd_sub(p, 0, L, sy.w(), ys, x, xs, out, os, dsc, batch, s);
     RCCHK(plan_ntt_range(p, false, 0, L, sy.w(), sy.w(), ys, ys, batch, s));
     return sub_scale(reinterpret_cast<const TowerScalar*>(dsc), x, sy.w(), out, xs, ys, os, batch, L, log_n, s);

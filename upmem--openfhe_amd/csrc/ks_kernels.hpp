@@ -269,12 +269,6 @@ struct SwArgs {
     u64 ql, pre, pre_p;  // pre: scalar on v mod ql first (1: none)
     u32 log_n, towers;
 };
-// NativeVectorT::SwitchModulus (mubintvecnat.cpp:111-136) of one value
-__device__ __forceinline__ u64 switch_mod1(u64 v, u64 om, u64 nm) {
-    if (v > (om >> 1)) v += nm > om ? nm - om : nm - (om % nm);
-    if (nm <= om && v >= nm) v = om <= 2 * nm ? csub(csub(v, nm), nm) : v % nm;  // v < om + nm
-    return v;
-}
 // two coefficients per thread (16-byte accesses); w = 1 (DropLastElementAndScale
 // with the reference's constants, where QlQlInvModqlDivqlModq = -qlInvModq)
 // skips the multiply

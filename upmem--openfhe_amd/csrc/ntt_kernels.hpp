@@ -951,8 +951,19 @@ __device__ __forceinline__ void cols_inv_b(u64 (&v)[CPT][E], bool (&b8)[E], cons
     }
 }
 
-template <int KA, bool INV, int CPT, bool SPQ>
-__global__ __launch_bounds__(256) void k_cols(PlanArgs P, const u64* src, u64* dst, u32 batch, u32 nwg) {
+// Rescaling source of the forward column pass (k_cols<.., SWS = true>):
+// element (b, t, pos) is SwitchModulus(last[b][pos]) from ql to q_t, times w_t
+// (tab[6 t + 1], Shoup constant at + 2; skipped when w_t = 1), so the lifted
+// towers are never written to HBM before their transform (keyswitch.hip,
+// DropLastElementAndScale / ModReduce in evaluation form).
+struct SwSrc {
+    const u64* last;
+    u64 lstride;
+    u64 ql;
+    const u64* tab;
+};
+template <int KA, bool INV, int CPT, bool SPQ, bool SWS = false>
+__global__ __launch_bounds__(256) void k_cols(PlanArgs P, const u64* src, u64* dst, u32 batch, u32 nwg, SwSrc S) {
     constexpr int E = 1 << KA;
     constexpr u32 N = 1u << (KA + 12);
     constexpr u32 CB = 16 / CPT;  // column blocks per polynomial
@@ -966,8 +977,29 @@ __global__ __launch_bounds__(256) void k_cols(PlanArgs P, const u64* src, u64* d
     const TowerConst tc = P.tc[t];
     const Mod<SPQ> M = load_mod<SPQ>(tc);
     u64 v[CPT][E];
+    if (SWS) {
+        const u64 w = S.tab[6 * t + 1], wp = S.tab[6 * t + 2];
+        const u64* lp = S.last + (u64)b * S.lstride + (inner - (u64)t * N);
 #pragma unroll
-    for (int k = 0; k < E; k++) {
+        for (int k = 0; k < E; k++) {
+            u64 lv[2];
+            if (CPT == 2) {
+                const u64x2 p = *reinterpret_cast<const u64x2*>(lp + (u64)k * 4096);
+                lv[0] = p.x;
+                lv[1] = p.y;
+            } else {
+                lv[0] = lp[(u64)k * 4096];
+            }
+#pragma unroll
+            for (int c = 0; c < CPT; c++) {
+                u64 e = switch_mod1(lv[c], S.ql, tc.q);
+                if (w != 1) e = shoup_canon(e, w, wp, tc.q);
+                v[c][k] = e;
+            }
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < E && !SWS; k++) {
         if (CPT == 2) {
             const u64x2 p = ld2_s(x + (u64)k * 4096);
             v[0][k] = p.x;

@@ -452,7 +452,14 @@ static void launch_cols_t(const PlanArgs& a, const u64* src, u64* dst, u32 batch
     // two columns per thread (16-byte accesses) while registers allow
     constexpr int CPT = KA <= 4 ? OFHE_COLS_CPT : 1;
     const u32 nwg = batch * a.towers * (16 / CPT);
-    hipLaunchKernelGGL((k_cols<KA, INV, CPT, SPQ>), dim3(nwg), dim3(256), 0, s, a, src, dst, batch, nwg);
+    hipLaunchKernelGGL((k_cols<KA, INV, CPT, SPQ>), dim3(nwg), dim3(256), 0, s, a, src, dst, batch, nwg, SwSrc{});
+}
+template <int KA, bool SPQ>
+static void launch_cols_sw(const PlanArgs& a, const SwSrc& S, u64* dst, u32 batch, hipStream_t s) {
+    constexpr int CPT = KA <= 4 ? OFHE_COLS_CPT : 1;
+    const u32 nwg = batch * a.towers * (16 / CPT);
+    hipLaunchKernelGGL((k_cols<KA, false, CPT, SPQ, true>), dim3(nwg), dim3(256), 0, s, a, (const u64*)nullptr, dst,
+                       batch, nwg, S);
 }
 
 template <bool SPQ>
@@ -573,6 +580,30 @@ int plan_ntt_range(ofhe_plan_t p, bool inverse, u32 t0, u32 count, const u64* sr
             launch_block<MODE_INV>(a, p->spq, src, dst, nullptr, batch, s, p->split8);
             if (p->log_n > 12) launch_colpass(ad, p->spq, p->split8, true, dst, dst, batch, s);
         }
+    }
+    return post_launch();
+}
+
+int plan_cols_switch(ofhe_plan_t p, u32 t0, u32 count, const u64* last, u64 lstride, u64 ql, const u64* tab, u64* y,
+                     u64 ystride, u32 batch, hipStream_t s) {
+    if (!p || !p->ctx) return fail(OFHE_ERR_STATE, "plan is NULL or destroyed");
+    if (p->log_n <= 12 || p->split8) return fail(OFHE_ERR_ARG, "plan_cols_switch: k_cols plans only");
+    if (((uintptr_t)last & 15) || (lstride & 1)) return fail(OFHE_ERR_ARG, "plan_cols_switch: misaligned source");
+    HIPCHK(hipSetDevice(p->ctx->device));
+    PlanArgs a = args_of(p, t0, count);
+    a.sstride = a.dstride = ystride;
+    const SwSrc S{last, lstride, ql, tab};
+    switch (p->log_n - 12) {
+#define CASE(K)                                                 \
+    case K:                                                     \
+        if (p->spq)                                             \
+            launch_cols_sw<K, true>(a, S, y, batch, s);         \
+        else                                                    \
+            launch_cols_sw<K, false>(a, S, y, batch, s);        \
+        break;
+        CASE(1) CASE(2) CASE(3) CASE(4) CASE(5)
+#undef CASE
+        default: break;
     }
     return post_launch();
 }
