@@ -84,11 +84,12 @@ int plan_ntt_fwd_sub(ofhe_plan_t p, u32 t0, u32 count, u64* y, u64 ystride, cons
                      u64 ostride, const u64* scal, u32 batch, hipStream_t s, int parts = 3);
 
 // Forward column pass (k_cols plans: 2^12 < N, not split8) of the towers
-// lifted from `last` ([batch] rows of N, stride lstride, modulus ql) and
+// lifted from `last` ([batch] rows of N, stride lstride, modulus ql; first
+// multiplied by pre mod ql unless pre = 1) and
 // scaled by tab[6 t + 1] (k_cols<.., SWS>), written to y; the block pass
 // (plan_ntt_fwd_sub parts = 2) follows.
-int plan_cols_switch(ofhe_plan_t p, u32 t0, u32 count, const u64* last, u64 lstride, u64 ql, const u64* tab, u64* y,
-                     u64 ystride, u32 batch, hipStream_t s);
+int plan_cols_switch(ofhe_plan_t p, u32 t0, u32 count, const u64* last, u64 lstride, u64 ql, u64 pre, const u64* tab,
+                     u64* y, u64 ystride, u32 batch, hipStream_t s);
 
 // ApproxSwitchCRTBasis launch (strides and output gap from A)
 int bconv_run(const BconvArgs& A, const u64* x, u64* out, u32 batch, hipStream_t s);

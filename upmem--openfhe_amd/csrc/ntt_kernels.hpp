@@ -961,6 +961,7 @@ struct SwSrc {
     u64 lstride;
     u64 ql;
     const u64* tab;
+    u64 pre, pre_p;  // scalar on last mod ql before the lift (ModReduce's negtInvModq), 1: none
 };
 template <int KA, bool INV, int CPT, bool SPQ, bool SWS = false>
 __global__ __launch_bounds__(256) void k_cols(PlanArgs P, const u64* src, u64* dst, u32 batch, u32 nwg, SwSrc S) {
@@ -992,7 +993,9 @@ __global__ __launch_bounds__(256) void k_cols(PlanArgs P, const u64* src, u64* d
             }
 #pragma unroll
             for (int c = 0; c < CPT; c++) {
-                u64 e = switch_mod1(lv[c], S.ql, tc.q);
+                u64 e = lv[c];
+                if (S.pre != 1) e = shoup_canon(e, S.pre, S.pre_p, S.ql);
+                e = switch_mod1(e, S.ql, tc.q);
                 if (w != 1) e = shoup_canon(e, w, wp, tc.q);
                 v[c][k] = e;
             }

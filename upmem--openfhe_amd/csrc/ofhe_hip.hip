@@ -452,7 +452,8 @@ static void launch_cols_t(const PlanArgs& a, const u64* src, u64* dst, u32 batch
     // two columns per thread (16-byte accesses) while registers allow
     constexpr int CPT = KA <= 4 ? OFHE_COLS_CPT : 1;
     const u32 nwg = batch * a.towers * (16 / CPT);
-    hipLaunchKernelGGL((k_cols<KA, INV, CPT, SPQ>), dim3(nwg), dim3(256), 0, s, a, src, dst, batch, nwg, SwSrc{});
+    hipLaunchKernelGGL((k_cols<KA, INV, CPT, SPQ>), dim3(nwg), dim3(256), 0, s, a, src, dst, batch, nwg,
+                       SwSrc{nullptr, 0, 0, nullptr, 1, 0});
 }
 template <int KA, bool SPQ>
 static void launch_cols_sw(const PlanArgs& a, const SwSrc& S, u64* dst, u32 batch, hipStream_t s) {
@@ -584,15 +585,16 @@ int plan_ntt_range(ofhe_plan_t p, bool inverse, u32 t0, u32 count, const u64* sr
     return post_launch();
 }
 
-int plan_cols_switch(ofhe_plan_t p, u32 t0, u32 count, const u64* last, u64 lstride, u64 ql, const u64* tab, u64* y,
-                     u64 ystride, u32 batch, hipStream_t s) {
+int plan_cols_switch(ofhe_plan_t p, u32 t0, u32 count, const u64* last, u64 lstride, u64 ql, u64 pre, const u64* tab,
+                     u64* y, u64 ystride, u32 batch, hipStream_t s) {
     if (!p || !p->ctx) return fail(OFHE_ERR_STATE, "plan is NULL or destroyed");
     if (p->log_n <= 12 || p->split8) return fail(OFHE_ERR_ARG, "plan_cols_switch: k_cols plans only");
     if (((uintptr_t)last & 15) || (lstride & 1)) return fail(OFHE_ERR_ARG, "plan_cols_switch: misaligned source");
     HIPCHK(hipSetDevice(p->ctx->device));
     PlanArgs a = args_of(p, t0, count);
     a.sstride = a.dstride = ystride;
-    const SwSrc S{last, lstride, ql, tab};
+    pre %= ql;
+    const SwSrc S{last, lstride, ql, tab, pre, pre == 1 ? 0 : shoup_pre(pre, ql)};
     switch (p->log_n - 12) {
 #define CASE(K)                                                 \
     case K:                                                     \
