@@ -37,10 +37,22 @@ __device__ __forceinline__ u64 mad32(u32 a, u32 b, u64 c) { return (u64)a * (u64
 
 __device__ __forceinline__ u64 csub(u64 x, u64 m) { return x >= m ? x - m : x; }
 
-// NativeVectorT::SwitchModulus (mubintvecnat.cpp:111-136) of one value
-__device__ __forceinline__ u64 switch_mod1(u64 v, u64 om, u64 nm) {
-    if (v > (om >> 1)) v += nm > om ? nm - om : nm - (om % nm);
-    if (nm <= om && v >= nm) v = om <= 2 * nm ? csub(csub(v, nm), nm) : v % nm;  // v < om + nm
+// the general remainder of switch_mod1 (old modulus more than twice the new
+// one): out of line, so the unrolled callers carry one copy of the division
+__device__ __noinline__ u64 umod64(u64 v, u64 m) { return v % m; }
+// NativeVectorT::SwitchModulus (mubintvecnat.cpp:111-136) of one value, with
+// the per-modulus-pair constants computed once (sw_mod) outside the loops
+struct SwMod {
+    u64 half, nm, diff;
+    bool down, small;  // nm <= om; om <= 2 nm (v < om + nm < 3 nm: two csubs)
+};
+__device__ __forceinline__ SwMod sw_mod(u64 om, u64 nm) {
+    const bool down = nm <= om;
+    return SwMod{om >> 1, nm, down ? nm - (om % nm) : nm - om, down, om <= 2 * nm};
+}
+__device__ __forceinline__ u64 switch_mod1(u64 v, const SwMod& m) {
+    if (v > m.half) v += m.diff;
+    if (m.down && v >= m.nm) v = m.small ? csub(csub(v, m.nm), m.nm) : umod64(v, m.nm);
     return v;
 }
 

@@ -780,7 +780,7 @@ static int rescale_run(ofhe_plan_t p, u32 towers, const u64* x, u64 xs, u64* out
     RCCHK(sy.alloc((size_t)batch * L * N * 8, s));
     RCCHK(plan_ntt_range(p, true, L, 1, x + (u64)L * N, sl.w(), xs, N, batch, s));
     const u64 ys = (u64)L * N;
-    if (log_n > 12 && !p->split8 && OFHE_RESCALE_FUSE) {
+    if (log_n > 12 && (!p->split8 || log_n == 16) && OFHE_RESCALE_FUSE) {
         // the lift happens in the column pass's loads (k_cols<.., SWS>): the
         // switched towers are never written to HBM before their transform
         RCCHK(plan_cols_switch(p, 0, L, sl.w(), N, ql, A.pre, dsw, sy.w(), ys, batch, s));

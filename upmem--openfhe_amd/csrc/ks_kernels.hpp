@@ -280,6 +280,7 @@ __global__ __launch_bounds__(256) void k_switch_scale(SwArgs A, u32 bpr) {
     if (j >= N) return;
     const u64* T = A.tab + 6 * (u64)t;
     const u64 q = T[0], w = T[1], wp = T[2], a = T[3], ap = T[4];
+    const SwMod sm = sw_mod(A.ql, q);
     const ulonglong2 lv = *reinterpret_cast<const ulonglong2*>(A.last + b * A.lstride + j);
     u64 r[2] = {lv.x, lv.y};
     ulonglong2 xv = make_ulonglong2(0, 0);
@@ -289,7 +290,7 @@ __global__ __launch_bounds__(256) void k_switch_scale(SwArgs A, u32 bpr) {
     for (int k = 0; k < 2; k++) {
         u64 v = r[k];
         if (A.pre != 1) v = shoup_canon(v, A.pre, A.pre_p, A.ql);
-        v = switch_mod1(v, A.ql, q);
+        v = switch_mod1(v, sm);
         if (w != 1) v = shoup_canon(v, w, wp, q);
         if (MODE == SW_AXPY) v = csub(shoup_canon(xs[k], a, ap, q) + v, q);
         if (MODE == SW_XPYA) v = shoup_canon(csub(xs[k] + v, q), a, ap, q);

@@ -697,6 +697,18 @@ __global__ __launch_bounds__(256, OFHE_KB_WAVES) void k_block(PlanArgs P, const 
     for (int k = 0; k < 16; k++) st_s(oblk + tid + 256 * k, v[k]);
 }
 
+// Rescaling source of the forward column pass (k_cols / k_tcols <.., SWS = true>):
+// element (b, t, pos) is SwitchModulus(last[b][pos]) from ql to q_t, times w_t
+// (tab[6 t + 1], Shoup constant at + 2; skipped when w_t = 1), so the lifted
+// towers are never written to HBM before their transform (keyswitch.hip,
+// DropLastElementAndScale / ModReduce in evaluation form).
+struct SwSrc {
+    const u64* last;
+    u64 lstride;
+    u64 ql;
+    const u64* tab;
+    u64 pre, pre_p;  // scalar on last mod ql before the lift (ModReduce's negtInvModq), 1: none
+};
 // ---------------------------------------------------------------------------
 // k_tcols: the first 8 forward stages (or the last 8 inverse stages) of an
 // N = 2^16 transform.  Element j = row * 256 + col; for a fixed col the 256
@@ -716,9 +728,9 @@ constexpr u32 TCOLS_W = OFHE_TCOLS_W;
 #define OFHE_TCOLS_PADF 1
 #endif
 static_assert(TCOLS_W == 16 || TCOLS_W == 32, "column tile width");
-template <bool INV, bool SPQ>
+template <bool INV, bool SPQ, bool SWS = false>
 __global__ __launch_bounds__(16 * TCOLS_W, OFHE_KB_WAVES) void k_tcols(PlanArgs P, const u64* src, u64* dst,
-                                                                       u32 batch, u32 nwg) {
+                                                                       u32 batch, u32 nwg, SwSrc SWA) {
     constexpr u32 N = 1u << 16, S = 256, W = TCOLS_W;
     // Exchange patterns p = tid + 16W k (round 1) and p = 16W h + W k + r
     // (round 2).  The inverse writes the second and reads the first: unpadded,
@@ -746,8 +758,21 @@ __global__ __launch_bounds__(16 * TCOLS_W, OFHE_KB_WAVES) void k_tcols(PlanArgs 
         const u64* tw = P.tw + (u64)t * N * 2;
         constexpr u32 RP = OFHE_TCOLS_PADF ? 16 * W + 16 : 16 * W;  // padded row pitch
         // round 1: rows h + 16k (p = tid + 16W k), stages m = 1..8
+        if (SWS) {
+            const u64 w = SWA.tab[6 * t + 1], wp = SWA.tab[6 * t + 2];
+            const SwMod sm = sw_mod(SWA.ql, tc.q);
+            const u64* lp = SWA.last + (u64)b * SWA.lstride + cb * W;
 #pragma unroll
-        for (int k = 0; k < 16; k++) v[k] = ld_s(x + (u64)(h + 16 * k) * S + r);
+            for (int k = 0; k < 16; k++) {
+                u64 e = lp[(u64)(h + 16 * k) * S + r];
+                if (SWA.pre != 1) e = shoup_canon(e, SWA.pre, SWA.pre_p, SWA.ql);
+                e = switch_mod1(e, sm);
+                v[k] = w != 1 ? shoup_canon(e, w, wp, tc.q) : e;
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < 16; k++) v[k] = ld_s(x + (u64)(h + 16 * k) * S + r);
+        }
         fwd_round16_canon(v, tw, 1, M);
 #pragma unroll
         for (int k = 0; k < 16; k++) lds[L1 + RP * k] = v[k];
@@ -951,18 +976,6 @@ __device__ __forceinline__ void cols_inv_b(u64 (&v)[CPT][E], bool (&b8)[E], cons
     }
 }
 
-// Rescaling source of the forward column pass (k_cols<.., SWS = true>):
-// element (b, t, pos) is SwitchModulus(last[b][pos]) from ql to q_t, times w_t
-// (tab[6 t + 1], Shoup constant at + 2; skipped when w_t = 1), so the lifted
-// towers are never written to HBM before their transform (keyswitch.hip,
-// DropLastElementAndScale / ModReduce in evaluation form).
-struct SwSrc {
-    const u64* last;
-    u64 lstride;
-    u64 ql;
-    const u64* tab;
-    u64 pre, pre_p;  // scalar on last mod ql before the lift (ModReduce's negtInvModq), 1: none
-};
 template <int KA, bool INV, int CPT, bool SPQ, bool SWS = false>
 __global__ __launch_bounds__(256) void k_cols(PlanArgs P, const u64* src, u64* dst, u32 batch, u32 nwg, SwSrc S) {
     constexpr int E = 1 << KA;
@@ -980,6 +993,7 @@ __global__ __launch_bounds__(256) void k_cols(PlanArgs P, const u64* src, u64* d
     u64 v[CPT][E];
     if (SWS) {
         const u64 w = S.tab[6 * t + 1], wp = S.tab[6 * t + 2];
+        const SwMod sm = sw_mod(S.ql, tc.q);
         const u64* lp = S.last + (u64)b * S.lstride + (inner - (u64)t * N);
 #pragma unroll
         for (int k = 0; k < E; k++) {
@@ -995,7 +1009,7 @@ __global__ __launch_bounds__(256) void k_cols(PlanArgs P, const u64* src, u64* d
             for (int c = 0; c < CPT; c++) {
                 u64 e = lv[c];
                 if (S.pre != 1) e = shoup_canon(e, S.pre, S.pre_p, S.ql);
-                e = switch_mod1(e, S.ql, tc.q);
+                e = switch_mod1(e, sm);
                 if (w != 1) e = shoup_canon(e, w, wp, tc.q);
                 v[c][k] = e;
             }

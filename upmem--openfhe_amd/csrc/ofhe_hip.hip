@@ -519,8 +519,9 @@ static void launch_tcols(const PlanArgs& a, bool spq, bool inv, const u64* src, 
         return;
     }
     const u32 nwg = batch * a.towers * (256 / TCOLS_W);
-#define LT(I, SP) \
-    hipLaunchKernelGGL((k_tcols<I, SP>), dim3(nwg), dim3(16 * TCOLS_W), 0, s, a, src, dst, batch, nwg)
+#define LT(I, SP)                                                                                 \
+    hipLaunchKernelGGL((k_tcols<I, SP>), dim3(nwg), dim3(16 * TCOLS_W), 0, s, a, src, dst, batch, nwg, \
+                       SwSrc{nullptr, 0, 0, nullptr, 1, 0})
     if (inv) {
         if (spq) LT(true, true); else LT(true, false);
     } else {
@@ -588,13 +589,23 @@ int plan_ntt_range(ofhe_plan_t p, bool inverse, u32 t0, u32 count, const u64* sr
 int plan_cols_switch(ofhe_plan_t p, u32 t0, u32 count, const u64* last, u64 lstride, u64 ql, u64 pre, const u64* tab,
                      u64* y, u64 ystride, u32 batch, hipStream_t s) {
     if (!p || !p->ctx) return fail(OFHE_ERR_STATE, "plan is NULL or destroyed");
-    if (p->log_n <= 12 || p->split8) return fail(OFHE_ERR_ARG, "plan_cols_switch: k_cols plans only");
+    if (p->log_n <= 12 || (p->split8 && p->log_n != 16)) return fail(OFHE_ERR_ARG, "plan_cols_switch: k_cols / k_tcols plans only");
     if (((uintptr_t)last & 15) || (lstride & 1)) return fail(OFHE_ERR_ARG, "plan_cols_switch: misaligned source");
     HIPCHK(hipSetDevice(p->ctx->device));
     PlanArgs a = args_of(p, t0, count);
     a.sstride = a.dstride = ystride;
     pre %= ql;
     const SwSrc S{last, lstride, ql, tab, pre, pre == 1 ? 0 : shoup_pre(pre, ql)};
+    if (p->split8) {  // N = 2^16: k_tcols
+        const u32 nwg = batch * a.towers * (256 / TCOLS_W);
+        if (p->spq)
+            hipLaunchKernelGGL((k_tcols<false, true, true>), dim3(nwg), dim3(16 * TCOLS_W), 0, s, a,
+                               (const u64*)nullptr, y, batch, nwg, S);
+        else
+            hipLaunchKernelGGL((k_tcols<false, false, true>), dim3(nwg), dim3(16 * TCOLS_W), 0, s, a,
+                               (const u64*)nullptr, y, batch, nwg, S);
+        return post_launch();
+    }
     switch (p->log_n - 12) {
 #define CASE(K)                                                 \
     case K:                                                     \
