@@ -297,6 +297,22 @@ int ofhe_hip_mod_reduce(ofhe_plan_t plan, uint32_t towers, const uint64_t* x, ui
                         uint64_t out_stride, int eval_form, uint64_t t, uint64_t neg_t_inv_modq,
                         const uint64_t* ql_inv_modq, uint32_t batch, void* stream);
 
+/* ---- BV key switching, digitSize = 0 (KeySwitchBV, keyswitch-bv.cpp:302-340) ----
+ * KeySwitchBV::EvalKeySwitchPrecomputeCore -> DCRTPolyImpl::CRTDecompose(0)
+ * (keyswitch-bv.cpp:308-312, dcrtpoly-impl.h:266-288): c [batch][towers][N]
+ * in evaluation form over plan towers 0..towers-1 -> digits
+ * [batch][towers][towers][N], digit i = tower i of c in coefficient form,
+ * SwitchModulus'd into every tower, in evaluation form. */
+int ofhe_hip_bv_precompute(ofhe_plan_t plan, uint32_t towers, const uint64_t* c, uint64_t* digits, uint32_t batch,
+                           void* stream);
+/* KeySwitchBV::EvalFastKeySwitchCore (keyswitch-bv.cpp:314-340): ct0 =
+ * sum_i bv[i] * d_i, ct1 = sum_i av[i] * d_i over the first `towers` towers of
+ * the keys key_b / key_a [towers][key_towers][N] (DropLastElements at lower
+ * levels); out0, out1 [batch][towers][N], evaluation form. */
+int ofhe_hip_bv_core(ofhe_plan_t plan, uint32_t towers, const uint64_t* digits, const uint64_t* key_b,
+                     const uint64_t* key_a, uint32_t key_towers, uint64_t* out0, uint64_t* out1, uint32_t batch,
+                     void* stream);
+
 /* ---- multi-GPU: evaluation-key broadcast over RCCL (xGMI) ----
  * the path shards by ciphertext batch with no exchange;
  * the one collective is the broadcast of the key-switching keys from a root

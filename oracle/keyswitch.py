@@ -380,3 +380,60 @@ def mod_reduce(x: np.ndarray, q, rq, eval_form: bool, t: int, neg_t_inv_modq: in
         m = O.eltwise("add", np.ascontiguousarray(x[:, i:i + 1]), tmp, [qi])  # m_vectors[i] += tmp
         out[:, i:i + 1] = _scale(m, [a[i]], [qi])                   # m_vectors[i] *= qlInvModq[i]
     return out
+
+
+# ---------------------------------------------------------------------------
+# BV key switching, digitSize = 0
+# ---------------------------------------------------------------------------
+def crt_decompose0(c: np.ndarray, q, rq) -> np.ndarray:
+    """DCRTPolyImpl::CRTDecompose(0), dcrtpoly-impl.h:266-288, for c [B][T][N]
+    in evaluation form: digit i = a copy of c (evaluation form) whose towers
+    k != i are tower i of the coefficient form, SwitchModulus'd to q_k and
+    transformed.  -> [B][T (digit)][T][N]."""
+    B, T, n = c.shape
+    coef = set_format(c, q, rq, False)                       # cp.SwitchFormat()
+    out = np.empty((B, T, T, n), np.uint64)
+    for i in range(T):
+        out[:, i] = c                                        # result[i] = *eval
+        for k in range(T):
+            if k != i:
+                tmp = switch_modulus(coef[:, i], int(q[i]), int(q[k]))[:, None]
+                out[:, i, k:k + 1] = set_format(tmp, [q[k]], [rq[k]], True)
+    return out
+
+
+def bv_fast_core(digits: np.ndarray, kb: np.ndarray, ka: np.ndarray, q):
+    """KeySwitchBV::EvalFastKeySwitchCore, keyswitch-bv.cpp:314-340: keys
+    [T][Tk][N] (the first T towers used, DropLastElements); digits [B][T][T][N]."""
+    B, T = digits.shape[0], digits.shape[1]
+    out0 = np.empty((B, T, digits.shape[3]), np.uint64)
+    out1 = np.empty_like(out0)
+    for b in range(B):
+        ct1 = O.eltwise("mul", ka[0:1, :T], digits[b, 0:1], q)            # av[0] *= digits[0]
+        ct0 = O.eltwise("mul", kb[0:1, :T], digits[b, 0:1], q)            # bv[0] *= digits[0]
+        for i in range(1, T):
+            ct0 = O.eltwise("add", ct0, O.eltwise("mul", kb[i:i + 1, :T], digits[b, i:i + 1], q), q)
+            ct1 = O.eltwise("add", ct1, O.eltwise("mul", ka[i:i + 1, :T], digits[b, i:i + 1], q), q)
+        out0[b], out1[b] = ct0[0], ct1[0]
+    return out0, out1
+
+
+def bv_keygen(q, rq, s_old, s_new, rng, err_bound=3):
+    """KeySwitchBV::KeySwitchGenInternal with digitSize = 0 (keyswitch-bv.cpp:
+    99-111): bv[i] = filtered_i - (a_i s_new + e_i), filtered_i = s_old in tower
+    i only; s_old, s_new in evaluation form [T][N].  Returns (kb, ka, e) with the
+    errors e [T][T][N] in evaluation form (noise scale 1)."""
+    T, n = len(q), s_old.shape[1]
+    kb = np.empty((T, T, n), np.uint64)
+    ka = np.empty_like(kb)
+    es = np.empty_like(kb)
+    for i in range(T):
+        a = np.stack([rng.integers(0, int(qk), size=n, dtype=np.uint64) for qk in q])
+        e = small_poly_eval(rng.integers(-err_bound, err_bound + 1, size=n), q, rq)[0]
+        filt = np.zeros((T, n), np.uint64)
+        filt[i] = s_old[i]
+        ase = O.eltwise("add", O.eltwise("mul", a[None], s_new[None], q), e[None], q)
+        kb[i] = O.eltwise("sub", filt[None], ase, q)[0]
+        ka[i] = a
+        es[i] = e
+    return kb, ka, es

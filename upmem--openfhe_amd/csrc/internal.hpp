@@ -91,6 +91,10 @@ int plan_ntt_fwd_sub(ofhe_plan_t p, u32 t0, u32 count, u64* y, u64 ystride, cons
 int plan_cols_switch(ofhe_plan_t p, u32 t0, u32 count, const u64* last, u64 lstride, u64 ql, u64 pre, const u64* tab,
                      u64* y, u64 ystride, u32 batch, hipStream_t s);
 
+// The block pass of a forward transform (y already through the column pass,
+// e.g. plan_cols_switch), in place; log_n > 12.
+int plan_ntt_fwd_block(ofhe_plan_t p, u32 t0, u32 count, u64* y, u64 ystride, u32 batch, hipStream_t s);
+
 // ApproxSwitchCRTBasis launch (strides and output gap from A)
 int bconv_run(const BconvArgs& A, const u64* x, u64* out, u32 batch, hipStream_t s);
 

@@ -838,3 +838,82 @@ int ofhe_hip_mod_reduce(ofhe_plan_t p, uint32_t towers, const uint64_t* x, uint6
     return rescale_run(p, towers, x, x_stride, out, out_stride, eval_form != 0, SW_XPYA, sw, sc, neg_t_inv_modq,
                        batch, pick(stream));
 }
+
+// ---------------------------------------------------------------------------
+// BV key switching with digitSize = 0 (KeySwitchBV, keyswitch-bv.cpp:302-340):
+// digit i of c is CRTDecompose(0)'s tower-i polynomial (dcrtpoly-impl.h:
+// 266-288): c_i in coefficient form lifted into every tower (SwitchModulus)
+// and transformed -- the fused lift + forward NTT of the rescaling path, one
+// launch pair per digit -- then the key inner product (k_bv_inner).
+// ---------------------------------------------------------------------------
+int ofhe_hip_bv_precompute(ofhe_plan_t p, uint32_t towers, const uint64_t* c, uint64_t* digits, uint32_t batch,
+                           void* stream) {
+    if (!p || !p->ctx) return fail(OFHE_ERR_STATE, "plan is NULL or destroyed");
+    if (!c || !digits || batch == 0) return fail(OFHE_ERR_ARG, "bad data argument");
+    if (towers < 1 || towers > p->towers) return fail(OFHE_ERR_ARG, "towers must be in [1, plan towers]");
+    if ((((uintptr_t)c | (uintptr_t)digits) & 15)) return fail(OFHE_ERR_ARG, "buffers must be 16-byte aligned");
+    HIPCHK(hipSetDevice(p->ctx->device));
+    hipStream_t s = pick(stream);
+    const u32 T = towers, log_n = p->log_n;
+    const u64 N = 1ull << log_n, TN = (u64)T * N;
+    std::vector<u64> sw(6 * (size_t)T, 0);
+    for (u32 k = 0; k < T; k++) {
+        const TowerScalar W = scalar_of(p->q[k], 1);
+        sw[6 * k] = p->q[k], sw[6 * k + 1] = W.s, sw[6 * k + 2] = W.sp;
+    }
+    const u64* dsw = nullptr;
+    RCCHK(plan_table(p, sw, &dsw));
+    Scratch sc;  // c in coefficient form
+    RCCHK(sc.alloc((size_t)batch * TN * 8, s));
+    RCCHK(plan_ntt_range(p, true, 0, T, c, sc.w(), TN, TN, batch, s));
+    const u64 dstride = (u64)T * TN;  // words per batch entry of digits
+    const bool fused = log_n > 12 && (!p->split8 || log_n == 16) && OFHE_RESCALE_FUSE;
+    const u32 bpr = (u32)((N / 2 + 255) / 256);
+    for (u32 i = 0; i < T; i++) {
+        u64* di = digits + (u64)i * TN;
+        if (fused) {
+            RCCHK(plan_cols_switch(p, 0, T, sc.w() + (u64)i * N, TN, p->q[i], 1, dsw, di, dstride, batch, s));
+            RCCHK(plan_ntt_fwd_block(p, 0, T, di, dstride, batch, s));
+            continue;
+        }
+        SwArgs A{};
+        A.last = sc.w() + (u64)i * N;
+        A.lstride = TN;
+        A.y = di;
+        A.ystride = dstride;
+        A.tab = dsw;
+        A.ql = p->q[i];
+        A.pre = 1;
+        A.log_n = log_n;
+        A.towers = T;
+        hipLaunchKernelGGL(k_switch_scale<SW_SCALE>, dim3(bpr * batch * T), dim3(256), 0, s, A, bpr);
+        RCCHK(post_launch());
+        RCCHK(plan_ntt_range(p, false, 0, T, di, di, dstride, dstride, batch, s));
+    }
+    return OFHE_OK;
+}
+
+int ofhe_hip_bv_core(ofhe_plan_t p, uint32_t towers, const uint64_t* digits, const uint64_t* key_b,
+                     const uint64_t* key_a, uint32_t key_towers, uint64_t* out0, uint64_t* out1, uint32_t batch,
+                     void* stream) {
+    if (!p || !p->ctx) return fail(OFHE_ERR_STATE, "plan is NULL or destroyed");
+    if (!digits || !key_b || !key_a || !out0 || !out1 || batch == 0) return fail(OFHE_ERR_ARG, "bad data argument");
+    if (towers < 1 || towers > p->towers) return fail(OFHE_ERR_ARG, "towers must be in [1, plan towers]");
+    if (key_towers < towers) return fail(OFHE_ERR_ARG, "key_towers smaller than towers");
+    if (towers > 256) return fail(OFHE_ERR_ARG, "at most 256 digits (128-bit accumulation)");
+    HIPCHK(hipSetDevice(p->ctx->device));
+    std::vector<u64> mu(3 * (size_t)towers);
+    for (u32 t = 0; t < towers; t++) {
+        const u128 m = ~(u128)0 / p->q[t];  // floor((2^128 - 1) / q) = floor(2^128 / q) for q not a power of two
+        mu[3 * t] = p->q[t], mu[3 * t + 1] = (u64)m, mu[3 * t + 2] = (u64)(m >> 64);
+    }
+    const u64* dmu = nullptr;
+    RCCHK(plan_table(p, mu, &dmu));
+    BvArgs A{digits, key_b, key_a, out0, out1, dmu, towers, towers, key_towers, p->log_n};
+    const u64 N = 1ull << p->log_n;
+    const u32 bpr = (u32)((N + 255) / 256);
+    const u64 blocks = (u64)bpr * batch * towers;
+    if (blocks >= (1ull << 31)) return fail(OFHE_ERR_ARG, "batch too large for one launch");
+    hipLaunchKernelGGL(k_bv_inner, dim3((u32)blocks), dim3(256), 0, pick(stream), A, bpr);
+    return post_launch();
+}

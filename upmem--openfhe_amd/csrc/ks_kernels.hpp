@@ -299,6 +299,47 @@ __global__ __launch_bounds__(256) void k_switch_scale(SwArgs A, u32 bpr) {
     st2_s(A.y + b * A.ystride + (u64)t * N + j, u64x2{r[0], r[1]});
 }
 
+// KeySwitchBV::EvalFastKeySwitchCore (keyswitch-bv.cpp:314-340):
+//   ct0 = sum_i bv[i] . d_i,  ct1 = sum_i av[i] . d_i   (per tower, mod q_t)
+// over `nd` digits.  One thread per (batch entry, tower, coefficient): the
+// products are summed exactly in 128 bits (nd <= 256 terms below 2^120) and
+// reduced once (BarrettUint128ModUint64, utilities-int.h:61-103) -- the
+// canonical residue the reference's per-term ModMul / ModAdd chain ends on.
+struct BvArgs {
+    const u64* d;     // [batch][nd][towers][N]
+    const u64* kb;    // [nd][key_towers][N]
+    const u64* ka;
+    u64* o0;          // [batch][towers][N]
+    u64* o1;
+    const u64* mu;    // [towers][3]: q, floor(2^128 / q) lo, hi
+    u32 nd, towers, key_towers, log_n;
+};
+__global__ __launch_bounds__(256) void k_bv_inner(BvArgs A, u32 bpr) {
+    const u32 row = blockIdx.x / bpr, b = row / A.towers, t = row % A.towers;
+    const u64 N = 1ull << A.log_n;
+    const u64 j = (u64)(blockIdx.x % bpr) * blockDim.x + threadIdx.x;
+    if (j >= N) return;
+    const u64 dstep = (u64)A.towers * N, kstep = (u64)A.key_towers * N;
+    const u64* dp = A.d + (u64)b * A.nd * dstep + (u64)t * N + j;
+    const u64* bp = A.kb + (u64)t * N + j;
+    const u64* ap = A.ka + (u64)t * N + j;
+    u64 l0 = 0, h0 = 0, l1 = 0, h1 = 0;
+    for (u32 i = 0; i < A.nd; i++) {
+        const u64 dv = ld_s(dp + i * dstep);
+        u64 lo, hi;
+        mul128(bp[i * kstep], dv, lo, hi);
+        l0 += lo;
+        h0 += hi + (l0 < lo);
+        mul128(ap[i * kstep], dv, lo, hi);
+        l1 += lo;
+        h1 += hi + (l1 < lo);
+    }
+    const u64 q = A.mu[3 * t], ml = A.mu[3 * t + 1], mh = A.mu[3 * t + 2];
+    const u64 o = (u64)b * A.towers * N + (u64)t * N + j;
+    st_s(A.o0 + o, barrett128(l0, h0, q, ml, mh));
+    st_s(A.o1 + o, barrett128(l1, h1, q, ml, mh));
+}
+
 // PolyImpl::AutomorphismTransform(k) (poly-impl.h:338-364).  One thread per
 // index j of one (batch, tower) row:
 //   evaluation form:  dst[rev(j)] = src[rev(((k (2j+1)) >> 1) mod n)]

@@ -621,6 +621,16 @@ int plan_cols_switch(ofhe_plan_t p, u32 t0, u32 count, const u64* last, u64 lstr
     return post_launch();
 }
 
+int plan_ntt_fwd_block(ofhe_plan_t p, u32 t0, u32 count, u64* y, u64 ystride, u32 batch, hipStream_t s) {
+    if (!p || !p->ctx) return fail(OFHE_ERR_STATE, "plan is NULL or destroyed");
+    if (p->log_n <= 12) return fail(OFHE_ERR_ARG, "plan_ntt_fwd_block: log_n > 12 only");
+    HIPCHK(hipSetDevice(p->ctx->device));
+    PlanArgs a = args_of(p, t0, count);
+    a.sstride = a.dstride = ystride;
+    launch_block<MODE_FWD>(a, p->spq, y, y, nullptr, batch, s, p->split8);
+    return post_launch();
+}
+
 int plan_ntt_fwd_sub(ofhe_plan_t p, u32 t0, u32 count, u64* y, u64 ystride, const u64* x, u64 xstride, u64* out,
                      u64 ostride, const u64* scal, u32 batch, hipStream_t s, int parts) {
     if (!p || !p->ctx) return fail(OFHE_ERR_STATE, "plan is NULL or destroyed");

@@ -107,6 +107,9 @@ _SIGS = {
                                                     ctypes.c_int, _vp, _vp, ctypes.c_uint32, _vp]),
     "ofhe_hip_mod_reduce": (ctypes.c_int, [_vp, ctypes.c_uint32, _vp, ctypes.c_uint64, _vp, ctypes.c_uint64,
                                            ctypes.c_int, ctypes.c_uint64, ctypes.c_uint64, _vp, ctypes.c_uint32, _vp]),
+    "ofhe_hip_bv_precompute": (ctypes.c_int, [_vp, ctypes.c_uint32, _vp, _vp, ctypes.c_uint32, _vp]),
+    "ofhe_hip_bv_core": (ctypes.c_int, [_vp, ctypes.c_uint32, _vp, _vp, _vp, ctypes.c_uint32, _vp, _vp,
+                                        ctypes.c_uint32, _vp]),
     "ofhe_hip_comm_unique_id": (ctypes.c_int, [_vp]),
     "ofhe_hip_comm_init": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int, _vp, ctypes.POINTER(_vp)]),
     "ofhe_hip_comm_destroy": (ctypes.c_int, [_vp]),
@@ -358,6 +361,18 @@ class NTTPlan:
         _check(lib().ofhe_hip_mod_reduce(self.handle, int(towers), _vp(x), int(x_stride), _vp(out), int(out_stride),
                                          1 if eval_form else 0, int(t), int(neg_t_inv_modq), _arr(a), int(batch),
                                          _vp(stream or None)))
+
+    # --- BV key switching, digitSize = 0 (keyswitch-bv.cpp:302-340) ---
+    def bv_precompute(self, towers: int, c: int, digits: int, batch: int = 1, stream: int = 0) -> None:
+        """CRTDecompose(0) of c [batch][towers][N] (evaluation form) -> digits [batch][towers][towers][N]."""
+        _check(lib().ofhe_hip_bv_precompute(self.handle, int(towers), _vp(c), _vp(digits), int(batch),
+                                            _vp(stream or None)))
+
+    def bv_core(self, towers: int, digits: int, key_b: int, key_a: int, key_towers: int, out0: int, out1: int,
+                batch: int = 1, stream: int = 0) -> None:
+        """EvalFastKeySwitchCore: out0 = sum_i kb[i] d_i, out1 = sum_i ka[i] d_i."""
+        _check(lib().ofhe_hip_bv_core(self.handle, int(towers), _vp(digits), _vp(key_b), _vp(key_a), int(key_towers),
+                                      _vp(out0), _vp(out1), int(batch), _vp(stream or None)))
 
     # --- the metric pipeline ---
     def ntt_mul_intt(self, a: int, b: int, c: int, batch: int = 1, stream: int = 0) -> None:
