@@ -372,6 +372,7 @@ def bench_pipeline(args):
         extras["configs3"] = bench_configs3(args, ctx, world, rank, dev)
         extras["keyswitch"] = bench_keyswitch(args, ctx, world, rank, dev, steps=args.ks_steps, warmup=2)
         extras["rescale"] = bench_rescale(args, ctx, world, rank, dev, steps=args.ks_steps, warmup=2)
+        extras["bv_keyswitch"] = bench_bv(args, ctx, world, rank, dev, steps=5, warmup=1)
         if rank == 0 and world == 1:
             extras["pcie_inclusive"] = (pcie_inclusive(plan, args.pcie_batch, args.pcie_chunks, dev)
                                         if args.pcie_chunks > 0 else None)
@@ -410,6 +411,7 @@ def bench_pipeline(args):
             "configs3": extras.get("configs3"),
             "keyswitch": extras.get("keyswitch"),
             "rescale": extras.get("rescale"),
+            "bv_keyswitch": extras.get("bv_keyswitch"),
             "configs0": extras.get("configs0"),
             "pcie_inclusive": extras.get("pcie_inclusive"),
             "build_id": build_id(),
@@ -561,6 +563,51 @@ def bench_rescale(args, ctx, world, rank, dev, steps, warmup):
             "ms_per_step": per * 1e3, "ms_per_step_events": ev_ms,
             "alg_hbm_gbs": B * (2 * T - 1) * n * 8 / per / 1e9,
             "note": "algorithmic bytes: read T towers, write T - 1 (8 B per word)"}
+
+
+# ---------------------------------------------------------------------------
+# BV key switching (digitSize = 0) on configs[4]'s ring and Q: N = 2^17, 48
+# towers, 48 digits; 2 ciphertext polynomials per GPU (digits: 2.4 GiB each)
+# ---------------------------------------------------------------------------
+def bench_bv(args, ctx, world, rank, dev, steps, warmup):
+    import torch
+    import torch.distributed as dist
+
+    import ofhe_hip as H
+    import shard
+
+    log_n, T, B = 17, 48, 2
+    n = 1 << log_n
+    q, rq = moduli_chain(log_n, T)
+    plan = H.NTTPlan(ctx, log_n, q, rq)
+    stream = torch.cuda.current_stream(dev)
+    sptr = stream.cuda_stream
+    b0, _ = shard.shard_batch(B * world, rank, world)
+    c = torch.empty((B, T, n), dtype=torch.int64, device=dev)
+    plan.fill_uniform(c.data_ptr(), B, 9, b0, sptr)
+    kb = torch.empty((T, T, n), dtype=torch.int64, device=dev)
+    ka = torch.empty_like(kb)
+    plan.fill_uniform(kb.data_ptr(), T, 10, 0, sptr)
+    plan.fill_uniform(ka.data_ptr(), T, 11, 0, sptr)
+    d = torch.empty((B, T, T, n), dtype=torch.int64, device=dev)
+    o0 = torch.empty((B, T, n), dtype=torch.int64, device=dev)
+    o1 = torch.empty_like(o0)
+
+    def step():
+        plan.bv_precompute(T, c.data_ptr(), d.data_ptr(), B, sptr)
+        plan.bv_core(T, d.data_ptr(), kb.data_ptr(), ka.data_ptr(), T, o0.data_ptr(), o1.data_ptr(), B, sptr)
+
+    elapsed, ev_ms = _timed(step, steps, warmup, stream, world, dev)
+    del c, kb, ka, d, o0, o1
+    plan.close()
+    torch.cuda.empty_cache()
+    if world > 1:
+        dist.barrier()
+    per = elapsed / steps
+    return {"workload": f"KeySwitchBV core, digitSize 0 (CRTDecompose + key inner product), N=2^17, {T} towers, "
+                        f"batch {B} per GPU",
+            "value": B * world / per, "unit": "keyswitch/s", "scaling": "weak", "steps": steps,
+            "ms_per_step": per * 1e3, "ms_per_step_events": ev_ms}
 
 
 # ---------------------------------------------------------------------------
