@@ -130,6 +130,14 @@ int ofhe_hip_ntt_inv_range(ofhe_plan_t plan, uint32_t t0, uint32_t count, const 
                            uint64_t* dst, uint64_t src_stride, uint64_t dst_stride, uint32_t batch,
                            void* stream);
 
+/* LeveledSHEBase::EvalMultCore for two 2-element ciphertexts
+ * (base-leveledshe.cpp:667-672), evaluation form, per (batch, tower) of plan:
+ *   out2 = c1 * d1,  out1 = c1 * d0 + c0 * d1,  out0 = d0 * c0
+ * (DCRTPoly operator* / += : Barrett ModMul, ModAdd), one pass over HBM.
+ * Outputs must not alias inputs. */
+int ofhe_hip_eval_mult_core(ofhe_plan_t plan, const uint64_t* c0, const uint64_t* c1, const uint64_t* d0,
+                            const uint64_t* d1, uint64_t* out0, uint64_t* out1, uint64_t* out2, uint32_t batch,
+                            void* stream);
 /* c = a (op) b element-wise per tower: NativeVectorT::ModMul (Barrett,
  * mubintvecnat.cpp:353-367 / .h:501-513), ModAdd (.cpp:245-264 / .h:426-432),
  * ModSub (.cpp:301-307).  c may alias a or b (the *Eq forms). */

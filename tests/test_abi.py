@@ -76,6 +76,7 @@ def test_argument_errors_without_device():
         L.ofhe_hip_drop_last_and_scale(null, 2, null, 32, null, 16, 1, q, q, 1, null),
         L.ofhe_hip_mod_reduce(null, 2, null, 32, null, 16, 1, 65537, 3, q, 1, null),
         L.ofhe_hip_bv_precompute(null, 2, null, null, 1, null),
+        L.ofhe_hip_eval_mult_core(null, null, null, null, null, null, null, null, 1, null),
         L.ofhe_hip_bv_core(null, 2, null, null, null, 2, null, null, 1, null),
         L.ofhe_hip_alloc_async(null, 8, ctypes.byref(vp()), null),
         L.ofhe_hip_bconv_create(null, 4, 1, 1, q, q, q, q, ctypes.byref(vp())),

@@ -28,6 +28,35 @@ __host__ __device__ constexpr int elt_unroll(int) { return OFHE_ELT_UNROLL; }
 #else
 __host__ __device__ constexpr int elt_unroll(int op) { return op == ELT_MUL ? 2 : 1; }
 #endif
+// LeveledSHEBase::EvalMultCore for two 2-element ciphertexts
+// (base-leveledshe.cpp:667-672): o2 = c1 d1, o1 = c1 d0 + c0 d1, o0 = d0 c0,
+// each product NativeVectorT::ModMul (Barrett, ubintnat.h:1399-1413) and the
+// sum ModAdd, in one pass: 32 B read and 24 B written per coefficient against
+// 120 B for the four products and the sum as separate vector ops.
+// One (batch, tower) row per bpr blocks, so the tower constants are
+// wave-uniform (scalar loads); two coefficients per thread.
+template <int V = 0>  // a template: this header is included by several translation units
+__global__ __launch_bounds__(256) void k_tensor2(const TowerConst* __restrict__ tcs, const u64* c0, const u64* c1,
+                                                 const u64* d0, const u64* d1, u64* o0, u64* o1, u64* o2, u32 bpr,
+                                                 u32 log_n, u32 towers) {
+    const u32 row = blockIdx.x / bpr;
+    const u64 j = 2 * ((u64)(blockIdx.x % bpr) * blockDim.x + threadIdx.x);
+    if (j >= (1ull << log_n)) return;
+    const u64 e = ((u64)row << log_n) + j;
+    const TowerConst tc = tcs[row % towers];
+    const u64x2 a0 = ld2_s(c0 + e), a1 = ld2_s(c1 + e), b0 = ld2_s(d0 + e), b1 = ld2_s(d1 + e);
+    u64x2 r0, r1, r2;
+    r2.x = barrett_ref(a1.x, b1.x, tc.q, tc.mu, tc.nshift);
+    r2.y = barrett_ref(a1.y, b1.y, tc.q, tc.mu, tc.nshift);
+    r1.x = modadd_fast(barrett_ref(a1.x, b0.x, tc.q, tc.mu, tc.nshift), barrett_ref(a0.x, b1.x, tc.q, tc.mu, tc.nshift), tc.q);
+    r1.y = modadd_fast(barrett_ref(a1.y, b0.y, tc.q, tc.mu, tc.nshift), barrett_ref(a0.y, b1.y, tc.q, tc.mu, tc.nshift), tc.q);
+    r0.x = barrett_ref(b0.x, a0.x, tc.q, tc.mu, tc.nshift);
+    r0.y = barrett_ref(b0.y, a0.y, tc.q, tc.mu, tc.nshift);
+    st2_s(o0 + e, r0);
+    st2_s(o1 + e, r1);
+    st2_s(o2 + e, r2);
+}
+
 template <int OP>
 __global__ __launch_bounds__(256) void k_eltwise(const TowerConst* __restrict__ tcs,
                                                  const u64* a, const u64* b, u64* c, u64 npairs,

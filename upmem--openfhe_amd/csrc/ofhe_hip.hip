@@ -913,6 +913,22 @@ static int eltwise(ofhe_plan_t p, const u64* a, const u64* b, u64* c, u32 batch,
     return post_launch();
 }
 
+int ofhe_hip_eval_mult_core(ofhe_plan_t p, const uint64_t* c0, const uint64_t* c1, const uint64_t* d0,
+                            const uint64_t* d1, uint64_t* out0, uint64_t* out1, uint64_t* out2, uint32_t batch,
+                            void* stream) {
+    int rc = check_common(p, batch);
+    if (rc) return rc;
+    if (!c0 || !c1 || !d0 || !d1 || !out0 || !out1 || !out2) return fail(OFHE_ERR_ARG, "NULL data pointer");
+    HIPCHK(hipSetDevice(p->ctx->device));
+    const u64 N = 1ull << p->log_n;
+    const u32 bpr = (u32)((N / 2 + 255) / 256);
+    const u64 blocks = (u64)bpr * batch * p->towers;
+    if (blocks >= (1ull << 31)) return fail(OFHE_ERR_ARG, "batch too large for one launch");
+    hipLaunchKernelGGL(k_tensor2<0>, dim3((u32)blocks), dim3(256), 0, pick(stream), p->d_tc, c0, c1, d0, d1, out0,
+                       out1, out2, bpr, p->log_n, p->towers);
+    return post_launch();
+}
+
 int ofhe_hip_modmul_vv(ofhe_plan_t p, const uint64_t* a, const uint64_t* b, uint64_t* c, uint32_t batch,
                        void* stream) {
     return eltwise<ELT_MUL>(p, a, b, c, batch, stream);

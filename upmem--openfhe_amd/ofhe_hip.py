@@ -110,6 +110,7 @@ _SIGS = {
     "ofhe_hip_bv_precompute": (ctypes.c_int, [_vp, ctypes.c_uint32, _vp, _vp, ctypes.c_uint32, _vp]),
     "ofhe_hip_bv_core": (ctypes.c_int, [_vp, ctypes.c_uint32, _vp, _vp, _vp, ctypes.c_uint32, _vp, _vp,
                                         ctypes.c_uint32, _vp]),
+    "ofhe_hip_eval_mult_core": (ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, ctypes.c_uint32, _vp]),
     "ofhe_hip_comm_unique_id": (ctypes.c_int, [_vp]),
     "ofhe_hip_comm_init": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int, _vp, ctypes.POINTER(_vp)]),
     "ofhe_hip_comm_destroy": (ctypes.c_int, [_vp]),
@@ -373,6 +374,12 @@ class NTTPlan:
         """EvalFastKeySwitchCore: out0 = sum_i kb[i] d_i, out1 = sum_i ka[i] d_i."""
         _check(lib().ofhe_hip_bv_core(self.handle, int(towers), _vp(digits), _vp(key_b), _vp(key_a), int(key_towers),
                                       _vp(out0), _vp(out1), int(batch), _vp(stream or None)))
+
+    # --- LeveledSHEBase::EvalMultCore, 2 x 2 elements (base-leveledshe.cpp:667-672) ---
+    def eval_mult_core(self, c0: int, c1: int, d0: int, d1: int, out0: int, out1: int, out2: int, batch: int = 1,
+                       stream: int = 0) -> None:
+        _check(lib().ofhe_hip_eval_mult_core(self.handle, _vp(c0), _vp(c1), _vp(d0), _vp(d1), _vp(out0), _vp(out1),
+                                             _vp(out2), int(batch), _vp(stream or None)))
 
     # --- the metric pipeline ---
     def ntt_mul_intt(self, a: int, b: int, c: int, batch: int = 1, stream: int = 0) -> None:
