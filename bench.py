@@ -134,6 +134,9 @@ def parse_args(argv=None):
                     help="nccl (RCCL, one GPU per rank); gloo = rehearsal of the N-rank path on one GPU")
     ap.add_argument("--launch-check", action="store_true",
                     help="start the ranks and report them (gloo, no GPU): checks the --gpus launcher")
+    ap.add_argument("--require-capi-comm", action="store_true",
+                    help="at N > 1, exit 3 (after printing the JSON line) unless every evaluation-key broadcast "
+                         "went through the C ABI's RCCL communicator (ofhe_hip_bcast_evalkey)")
     return ap.parse_args(argv)
 
 
@@ -158,20 +161,50 @@ def launch_ranks(n: int) -> int:
     return subprocess.call(cmd, env=env)
 
 
-def launch_check():
-    """Each rank joins a gloo group; rank 0 prints the ranks that came up."""
+def capi_status(records, world):
+    """Top-level summary of how the evaluation keys travelled: capi is True only
+    when every broadcast of the run used ofhe_hip_bcast_evalkey (None at N = 1:
+    nothing is broadcast); reasons name each fallback."""
+    recs = {k: v for k, v in records.items() if v}
+    if world <= 1 or not recs:
+        return {"capi": None, "reasons": [], "broadcasts": sorted(recs)}
+    bad = {k: v.get("backend") for k, v in recs.items() if not v.get("capi")}
+    return {"capi": not bad, "reasons": [f"{k}: {why}" for k, why in sorted(bad.items())],
+            "broadcasts": sorted(recs)}
+
+
+def capi_exit_code(status, require: bool) -> int:
+    """--require-capi-comm: 3 when a broadcast fell back (the JSON is printed first)."""
+    return 3 if require and status.get("capi") is False else 0
+
+
+def launch_check(args):
+    """Each rank joins a gloo group; rank 0 prints the ranks that came up and
+    how the key broadcaster came up (no GPU: the C-ABI communicator cannot, so
+    the ranks fall back together; --require-capi-comm then exits 3)."""
+    import torch
     import torch.distributed as dist
+
+    import shard
 
     dist.init_process_group("gloo")
     world, rank = dist.get_world_size(), dist.get_rank()
     info = [None] * world
     dist.all_gather_object(info, {"rank": rank, "pid": os.getpid(), "local_rank": int(os.environ["LOCAL_RANK"])})
+    bfn, backend, comm = shard.key_broadcaster(None, rank, world)
+    key = torch.arange(64, dtype=torch.int64) if rank == 0 else torch.zeros(64, dtype=torch.int64)
+    bfn(key, 0)
+    rec = {"backend": backend, "capi": comm is not None, "verified": shard.same_on_all_ranks(key)}
+    status = capi_status({"launch_check": rec}, world)
     if rank == 0:
         print(json.dumps({"launch_check": True, "n_gpus": world, "ranks": [i["rank"] for i in info],
-                          "local_ranks": [i["local_rank"] for i in info], "pids": [i["pid"] for i in info]}),
-              flush=True)
+                          "local_ranks": [i["local_rank"] for i in info], "pids": [i["pid"] for i in info],
+                          "evalkey_broadcast": rec, "evalkey_broadcast_capi": status}), flush=True)
+    if comm is not None:
+        comm.close()
     dist.barrier()
     dist.destroy_process_group()
+    return capi_exit_code(status, args.require_capi_comm)
 
 
 def main():
@@ -186,10 +219,10 @@ def main():
         if env_world is None:
             print(json.dumps({"launch_check": True, "n_gpus": 1, "ranks": [0], "pids": [os.getpid()]}))
             return
-        return launch_check()
+        sys.exit(launch_check(args))
     if args.workload == "keyswitch":
-        return bench_keyswitch_main(args)
-    return bench_pipeline(args)
+        sys.exit(bench_keyswitch_main(args))
+    sys.exit(bench_pipeline(args))
 
 
 # ---------------------------------------------------------------------------
@@ -315,7 +348,7 @@ def bench_pipeline(args):
         bfn(key, 0)
         torch.cuda.synchronize()
         bcast = {"bytes": key.numel() * 8, "ms": (time.perf_counter() - t0) * 1e3, "backend": backend,
-                 "verified": shard.same_on_all_ranks(key)}
+                 "capi": comm is not None, "verified": shard.same_on_all_ranks(key)}
         del key
 
     def step():
@@ -379,6 +412,8 @@ def bench_pipeline(args):
             extras["configs0"] = bench_configs0(ctx)
             extras["cpu_baseline"] = cpu_baseline(args, qs, roots, log_n, T) if args.cpu_seconds > 0 else None
 
+    status = capi_status({"headline": bcast, "keyswitch": (extras.get("keyswitch") or {}).get("evalkey_broadcast")},
+                         world)
     if rank == 0:
         out = {
             "metric": METRIC,
@@ -408,6 +443,7 @@ def bench_pipeline(args):
             "cpu_baseline": extras.get("cpu_baseline"),
             "parity_spot_check": parity,
             "evalkey_broadcast": bcast,
+            "evalkey_broadcast_capi": status,
             "configs3": extras.get("configs3"),
             "keyswitch": extras.get("keyswitch"),
             "rescale": extras.get("rescale"),
@@ -423,6 +459,7 @@ def bench_pipeline(args):
             comm.close()
         dist.barrier()
         dist.destroy_process_group()
+    return capi_exit_code(status, args.require_capi_comm)
 
 
 def make_roofline(pipe_ms, kernels_ms, coeffs_rank, log_n, T, B):
@@ -643,7 +680,8 @@ def bench_keyswitch(args, ctx, world, rank, dev, steps, warmup, with_stages=Fals
         bfn, backend, comm = shard.key_broadcaster(ctx, rank, world)
         bfn(kb, 0)
         bfn(ka, 0)
-        key_bcast = {"backend": backend, "verified": shard.same_on_all_ranks(kb) and shard.same_on_all_ranks(ka)}
+        key_bcast = {"backend": backend, "capi": comm is not None,
+                     "verified": shard.same_on_all_ranks(kb) and shard.same_on_all_ranks(ka)}
     o0 = torch.empty((B, sq, n), dtype=torch.int64, device=dev)
     o1 = torch.empty_like(o0)
 
@@ -710,13 +748,16 @@ def bench_keyswitch_main(args):
 
     ctx = H.Context(local)
     out = bench_keyswitch(args, ctx, world, rank, dev, steps=args.steps, warmup=args.warmup, with_stages=True)
+    status = capi_status({"keyswitch": out.get("evalkey_broadcast")}, world)
     if rank == 0:
         out.update({"n_gpus": world, "higher_is_better": True, "vs_baseline": None, "dtype": "u64",
-                    "data": "synthetic: splitmix64 ciphertext and key residues (SURVEY.md §8(d) seeds)"})
+                    "data": "synthetic: splitmix64 ciphertext and key residues (SURVEY.md §8(d) seeds)",
+                    "evalkey_broadcast_capi": status})
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+    return capi_exit_code(status, args.require_capi_comm)
 
 
 # ---------------------------------------------------------------------------

@@ -89,6 +89,10 @@ int ofhe_hip_copy_to_host(ofhe_ctx_t ctx, void* dst, const void* src, size_t byt
 int ofhe_hip_copy_device(ofhe_ctx_t ctx, void* dst, const void* src, size_t bytes, void* stream);
 /* PimManager::start_kernel is synchronous (PimManager.h:68); here explicit. */
 int ofhe_hip_sync(ofhe_ctx_t ctx, void* stream);
+/* Return all but keep_bytes of the context's stream-ordered pool (scratch and
+ * ofhe_hip_alloc_async blocks kept across synchronisations) to the device; the
+ * reference frees DPU memory per call (PimManager::deallocate, PimManager.h:83-85). */
+int ofhe_hip_trim(ofhe_ctx_t ctx, size_t keep_bytes);
 
 /* ---- NTT plan: replaces ChineseRemainderTransformFTTNat::PreCompute and
  *      its static twiddle maps (transformnat-impl.h:708-763,
@@ -283,7 +287,9 @@ int ofhe_hip_automorphism(ofhe_plan_t plan, uint32_t k, int eval_form, const uin
 /* ---- rescaling (callers of the path one tower down) ----
  * x: [batch][towers][N] (x_stride words per batch entry) over plan towers
  * 0..towers-1, canonical, all in evaluation form (eval_form != 0) or all in
- * coefficient form; out: [batch][towers-1][N] (out_stride), may alias x.
+ * coefficient form; out: [batch][towers-1][N] (out_stride).  out may be x
+ * itself only with out_stride == x_stride (in place); any other overlap of
+ * the two ranges is rejected with OFHE_ERR_ARG.
  * DCRTPolyImpl::DropLastElementAndScale (dcrtpoly-impl.h:746-768), CKKS / BFV
  * rescaling with ql_ql_inv_modql_divql_modq[i] and ql_inv_modq[i], i <
  * towers-1 (ckksrns-cryptoparameters.cpp:72-86):

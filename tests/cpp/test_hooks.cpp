@@ -34,6 +34,7 @@ void oracle_approx_switch_crt_basis(const uint64_t* x, uint64_t* out, uint64_t n
 }
 
 namespace mock {
+enum class Format { EVALUATION = 0, COEFFICIENT = 1 };  // the reference's enumerators (utils/inttypes.h)
 struct NativeInteger {  // NativeIntegerT<uint64_t>: one word
     uint64_t m_value = 0;
     uint64_t ConvertToInt() const { return m_value; }
@@ -44,15 +45,52 @@ struct ILNativeParams {
     const NativeInteger& GetModulus() const { return modulus; }
     const NativeInteger& GetRootOfUnity() const { return root; }
     uint32_t GetRingDimension() const { return ring; }
+    uint32_t GetCyclotomicOrder() const { return 2 * ring; }  // power-of-two cyclotomic
 };
+int g_cpu_switches = 0;  // towers transformed by the CPU loop (PolyImpl::SwitchFormat)
 struct PolyImpl {
     std::shared_ptr<ILNativeParams> params;
     std::vector<NativeInteger> values;
+    Format m_format = Format::COEFFICIENT;
     const std::shared_ptr<ILNativeParams>& GetParams() const { return params; }
     NativeInteger& operator[](uint32_t i) { return values[i]; }
     const NativeInteger& operator[](uint32_t i) const { return values[i]; }
+    Format GetFormat() const { return m_format; }
+    void OverrideFormat(Format f) { m_format = f; }  // poly.h:179
+    void SwitchFormat();                              // poly-impl.h:412-432, on the oracle
+};
+// DCRTPolyImpl with the RUN_ON_HIP SwitchFormat exactly as INTEGRATION.md §3
+// shows it for dcrtpoly-impl.h:2516-2523: the hook, else the reference loop
+struct DCRTPolyImpl {
+    Format m_format = Format::COEFFICIENT;
+    std::vector<PolyImpl> m_vectors;
+    void SwitchFormat() {
+        m_format = (m_format == Format::COEFFICIENT) ? Format::EVALUATION : Format::COEFFICIENT;
+        if (ofhe::hooks::SwitchFormat(m_vectors)) return;
+        size_t size{m_vectors.size()};
+        for (size_t i = 0; i < size; ++i) m_vectors[i].SwitchFormat();
+    }
 };
 }  // namespace mock
+
+void mock::PolyImpl::SwitchFormat() {
+    const uint32_t n = params->ring;
+    uint32_t log_n = 0;
+    while ((1u << log_n) < n) log_n++;
+    std::vector<uint64_t> tab(n), tp(n), it(n), ip(n), coi(log_n + 1), cp(log_n + 1), x(n);
+    const uint64_t q = params->modulus.m_value;
+    oracle_ntt_tables(n, q, params->root.m_value, tab.data(), tp.data(), it.data(), ip.data(), coi.data(), cp.data());
+    for (uint32_t i = 0; i < n; i++) x[i] = values[i].m_value;
+    if (m_format == Format::COEFFICIENT) {
+        oracle_ntt_fwd(x.data(), n, q, tab.data(), tp.data());
+        m_format = Format::EVALUATION;
+    } else {
+        oracle_ntt_inv(x.data(), n, q, it.data(), ip.data(), coi[log_n], cp[log_n]);
+        m_format = Format::COEFFICIENT;
+    }
+    for (uint32_t i = 0; i < n; i++) values[i].m_value = x[i];
+    g_cpu_switches++;
+}
 
 static int g_fail = 0;
 #define CHECK(c, msg)                                      \
@@ -88,22 +126,45 @@ int main() {
     std::vector<uint64_t> p(all.begin() + T, all.end()), rp(roots.begin() + T, roots.end());
     std::mt19937_64 rng(77);
     try {
-        // SwitchFormat both ways, against the oracle's per-tower transforms
+        // DCRTPolyImpl::SwitchFormat through the hook (N = 2^12: the device)
+        // against the reference's own per-tower loop on the oracle
         auto a = towers(n, q, r, rng);
         auto a0 = a;
-        ofhe::hooks::SwitchFormat(a, true);
-        bool ok = true;
-        for (uint32_t t = 0; t < T; t++) {
-            std::vector<uint64_t> tab(n), tp(n), it(n), ip(n), coi(log_n + 1), cp(log_n + 1), x = words(a0[t]);
-            oracle_ntt_tables(n, q[t], r[t], tab.data(), tp.data(), it.data(), ip.data(), coi.data(), cp.data());
-            oracle_ntt_fwd(x.data(), n, q[t], tab.data(), tp.data());
-            ok = ok && x == words(a[t]);
+        {
+            mock::DCRTPolyImpl d{mock::Format::COEFFICIENT, a}, ref{mock::Format::COEFFICIENT, a};
+            mock::g_cpu_switches = 0;
+            d.SwitchFormat();
+            CHECK(mock::g_cpu_switches == 0, "N = 2^12 SwitchFormat ran on the device");
+            for (auto& t : ref.m_vectors) t.SwitchFormat();
+            bool ok = d.m_format == mock::Format::EVALUATION;
+            for (uint32_t t = 0; t < T; t++)
+                ok = ok && words(d.m_vectors[t]) == words(ref.m_vectors[t]) &&
+                     d.m_vectors[t].GetFormat() == mock::Format::EVALUATION;
+            CHECK(ok, "hooks::SwitchFormat (forward) vs oracle, formats flipped");
+            a = d.m_vectors;
+            d.SwitchFormat();
+            ok = d.m_format == mock::Format::COEFFICIENT && mock::g_cpu_switches == (int)T;  // T: the ref loop above
+            for (uint32_t t = 0; t < T; t++)
+                ok = ok && words(d.m_vectors[t]) == words(a0[t]) && d.m_vectors[t].GetFormat() == mock::Format::COEFFICIENT;
+            CHECK(ok, "hooks::SwitchFormat round trip");
         }
-        CHECK(ok, "hooks::SwitchFormat (forward) vs oracle");
-        ofhe::hooks::SwitchFormat(a, false);
-        ok = true;
-        for (uint32_t t = 0; t < T; t++) ok = ok && words(a[t]) == words(a0[t]);
-        CHECK(ok, "hooks::SwitchFormat round trip");
+        // small ring (binfhe-sized N = 2^10): the hook declines, the reference
+        // loop runs, the format still flips and the values equal the oracle's
+        {
+            const uint32_t ns = 1u << 10;
+            std::vector<uint64_t> qs(3), rs(3);
+            oracle_moduli_chain(60, 2 * ns, 3, qs.data(), rs.data());
+            auto sm = towers(ns, qs, rs, rng);
+            mock::DCRTPolyImpl d{mock::Format::COEFFICIENT, sm}, ref{mock::Format::COEFFICIENT, sm};
+            mock::g_cpu_switches = 0;
+            d.SwitchFormat();
+            bool ok = mock::g_cpu_switches == 3 && d.m_format == mock::Format::EVALUATION;
+            for (auto& t : ref.m_vectors) t.SwitchFormat();
+            for (size_t t = 0; t < 3; t++) ok = ok && words(d.m_vectors[t]) == words(ref.m_vectors[t]);
+            CHECK(ok, "N = 2^10 SwitchFormat takes the CPU loop and flips m_format");
+            CHECK(!ofhe::hooks::device_switch_format(d.m_vectors), "device_switch_format(N = 2^10) is false");
+        }
+        bool ok = true;
         // element-wise *=, +=, -= against the oracle
         auto b = towers(n, q, r, rng);
         for (int op = 0; op < 3; op++) {

@@ -66,3 +66,33 @@ def test_roofline_uses_only_matching_counters(tmp_path, monkeypatch):
     pm["config"]["batch"] = 256
     f.write_text(json.dumps(pm))
     assert bench.make_roofline(13.5, kms, coeffs, 16, 16, 1024)["valu"] is None
+
+
+def test_require_capi_comm_fires_on_fallback():
+    """--require-capi-comm: the ranks print their JSON line, then exit non-zero
+    when the evaluation key did not travel through ofhe_hip_bcast_evalkey (on
+    a CPU box the C-ABI communicator cannot come up, so the ranks fall back to
+    gloo together).  Without the flag the same run succeeds."""
+    for flag, ok in (([], True), (["--require-capi-comm"], False)):
+        r = subprocess.run([sys.executable, BENCH, "--gpus", "2", "--launch-check"] + flag, capture_output=True,
+                           text=True, timeout=240, env=_env())
+        line = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+        assert len(line) == 1, (r.stdout, r.stderr[-2000:])
+        out = json.loads(line[0])
+        st = out["evalkey_broadcast_capi"]
+        assert st["capi"] is False and st["reasons"] and "torch.distributed gloo" in st["reasons"][0]
+        assert out["evalkey_broadcast"]["verified"] is True
+        assert (r.returncode == 0) == ok, (flag, r.returncode, r.stderr[-2000:])
+
+
+def test_capi_status_bookkeeping():
+    import bench
+
+    assert bench.capi_status({"headline": None}, 1)["capi"] is None
+    good = {"backend": "ofhe_hip_bcast_evalkey (RCCL)", "capi": True}
+    bad = {"backend": "torch.distributed nccl (C-ABI comm: x)", "capi": False}
+    assert bench.capi_status({"headline": good, "keyswitch": good}, 8)["capi"] is True
+    st = bench.capi_status({"headline": good, "keyswitch": bad}, 8)
+    assert st["capi"] is False and st["reasons"] == ["keyswitch: torch.distributed nccl (C-ABI comm: x)"]
+    assert bench.capi_exit_code(st, True) == 3 and bench.capi_exit_code(st, False) == 0
+    assert bench.capi_exit_code(bench.capi_status({"headline": good}, 2), True) == 0

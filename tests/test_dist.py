@@ -153,3 +153,45 @@ def test_two_rank_sharded_keyswitch_with_broadcast_key():
         assert p.exitcode == 0
     assert sorted(r[0] for r in res) == [0, 1]
     assert all(r[1] is True for r in res), res
+
+
+def _uid_fail_worker(rank, world, port, q):
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        try:
+            import ofhe_hip as H
+
+            def no_uid():
+                raise H.MathError("ncclGetUniqueId refused (test)")
+
+            H.comm_unique_id = no_uid  # rank 0's id fails before its broadcast
+            bfn, label, comm = shard.key_broadcaster(object(), rank, world)
+            key = torch.arange(32, dtype=torch.int64) if rank == 0 else torch.zeros(32, dtype=torch.int64)
+            bfn(key, 0)
+            q.put((rank, comm is None, label, bool(torch.equal(key, torch.arange(32, dtype=torch.int64)))))
+        finally:
+            dist.destroy_process_group()
+    except Exception as e:
+        q.put((rank, False, repr(e), False))
+        raise
+
+
+def test_two_rank_unique_id_failure_falls_back_without_hanging():
+    """rank 0's ofhe_hip_comm_unique_id failing must not leave the
+    peers in broadcast_object_list while rank 0 enters the all_reduce: every
+    rank reaches the fallback, the key still arrives, the reason is named."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_uid_fail_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert sorted(r[0] for r in res) == [0, 1]
+    for rank, fell_back, label, key_ok in res:
+        assert fell_back and key_ok, res
+        assert "torch.distributed gloo" in label and "unique id failed on rank 0" in label, label

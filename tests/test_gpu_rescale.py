@@ -89,3 +89,29 @@ def test_rescale_lower_level_and_edges(hip):
         plan.drop_last_and_scale(1, dx.data_ptr(), n, dx.data_ptr(), n, True, c, a, B, stream())
     with pytest.raises(H.MathError):  # qlInvModq must be invertible in evaluation form
         plan.drop_last_and_scale(T, dx.data_ptr(), T * n, dx.data_ptr(), T * n, True, c, [0] * (T - 1), B, stream())
+
+
+def test_rescale_rejects_unsafe_aliasing(hip):
+    """out may be x only in place with equal strides.  A packed
+    output over the input (out_stride = (towers-1)N < x_stride, batch >= 2)
+    would overwrite towers of the previous entry that other workgroups still
+    read, so it is refused; so is a partial overlap.  In place with equal
+    strides still matches the oracle, and the context's scratch pool can be
+    trimmed afterwards."""
+    H, ctx = hip
+    log_n, T, B = 13, 4, 3
+    n, q, r, x = _case(log_n, T, B, 99)
+    c, a = K.rescale_tables(q)
+    plan = H.NTTPlan(ctx, log_n, q, r)
+    dx = dev(x)
+    for ev in (True, False):
+        with pytest.raises(H.MathError, match="overlaps"):
+            plan.drop_last_and_scale(T, dx.data_ptr(), T * n, dx.data_ptr(), (T - 1) * n, ev, c, a, B, stream())
+        with pytest.raises(H.MathError, match="overlaps"):
+            plan.drop_last_and_scale(T, dx.data_ptr(), T * n, dx.data_ptr() + 8 * n, T * n, ev, c, a, B, stream())
+        with pytest.raises(H.MathError, match="overlaps"):
+            plan.mod_reduce(T, dx.data_ptr(), T * n, dx.data_ptr(), (T - 1) * n, ev, 2, 1, a, B, stream())
+    assert np.array_equal(host(dx), x)  # nothing was launched
+    plan.drop_last_and_scale(T, dx.data_ptr(), T * n, dx.data_ptr(), T * n, True, c, a, B, stream())
+    assert np.array_equal(host(dx)[:, :T - 1], K.drop_last_and_scale(x, q, r, True, c, a))
+    ctx.trim(0)

@@ -95,6 +95,15 @@ int plan_cols_switch(ofhe_plan_t p, u32 t0, u32 count, const u64* last, u64 lstr
 // e.g. plan_cols_switch), in place; log_n > 12.
 int plan_ntt_fwd_block(ofhe_plan_t p, u32 t0, u32 count, u64* y, u64 ystride, u32 batch, hipStream_t s);
 
+// Table upload for the one-time (cache-miss / setup) paths: a pageable
+// hipMemcpy followed by a wait on the null stream it ran on, so the words are
+// in device memory before the call returns and any later launch, on any
+// stream, reads them (a pageable copy may return before its DMA has landed).
+inline hipError_t upload_blocking(void* dst, const void* src, size_t bytes) {
+    hipError_t e = hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice);
+    return e == hipSuccess ? hipStreamSynchronize(nullptr) : e;
+}
+
 // ApproxSwitchCRTBasis launch (strides and output gap from A)
 int bconv_run(const BconvArgs& A, const u64* x, u64* out, u32 batch, hipStream_t s);
 
@@ -102,6 +111,7 @@ int bconv_run(const BconvArgs& A, const u64* x, u64* out, u32 batch, hipStream_t
 
 struct ofhe_ctx_s {
     int device = 0;
+    hipMemPool_t pool = nullptr;  // stream-ordered scratch + ofhe_hip_alloc_async (null: the default pool)
     std::atomic<int> live{1};
 };
 

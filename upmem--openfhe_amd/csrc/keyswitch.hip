@@ -40,6 +40,7 @@ using namespace ofhe;
 #define OFHE_KS_NSIDE 2
 #endif
 constexpr int KS_NSIDE = OFHE_KS_NSIDE;
+static_assert(KS_NSIDE >= 2, "KeySwitchCore's two ModDowns use side streams 0 and 1");
 
 namespace {
 
@@ -81,13 +82,15 @@ int sub_scale(const TowerScalar* d, const u64* x, const u64* y, u64* out, u64 xs
     return post_launch();
 }
 
-// Stream-ordered scratch: freed on the stream when the owner goes out of scope.
+// Stream-ordered scratch from the context's pool: freed on the stream when the
+// owner goes out of scope.
 struct Scratch {
     void* p = nullptr;
     hipStream_t s = nullptr;
-    int alloc(size_t bytes, hipStream_t st) {
+    int alloc(size_t bytes, hipStream_t st, ofhe_ctx_t ctx) {
         s = st;
-        hipError_t e = hipMallocAsync(&p, bytes ? bytes : 8, st);
+        hipError_t e = ctx->pool ? hipMallocFromPoolAsync(&p, bytes ? bytes : 8, ctx->pool, st)
+                                 : hipMallocAsync(&p, bytes ? bytes : 8, st);
         if (e != hipSuccess) return fail(OFHE_ERR_NOMEM, std::string("scratch: ") + hipGetErrorString(e));
         return OFHE_OK;
     }
@@ -119,8 +122,8 @@ int mod_down_run(const ModDownArgs& A, const u64* x, u64 xstride, u64* out, u64 
     const u32 log_n = A.plan_q->log_n;
     const u64 N = 1ull << log_n;
     Scratch sp, sq;
-    RCCHK(sp.alloc((size_t)batch * A.size_p * N * 8, s));
-    RCCHK(sq.alloc((size_t)batch * A.size_q * N * 8, s));
+    RCCHK(sp.alloc((size_t)batch * A.size_p * N * 8, s, A.plan_q->ctx));
+    RCCHK(sq.alloc((size_t)batch * A.size_q * N * 8, s, A.plan_q->ctx));
     const u64 ps = A.size_p * N, qs = A.size_q * N;
     // partP: P towers to coefficient form (dcrtpoly-impl.h:1147-1153)
     RCCHK(plan_ntt_range(A.plan_p, true, A.p0, A.size_p, x + qs, sp.w(), xstride, ps, batch, s));
@@ -154,8 +157,8 @@ int mod_down_run2(const ModDownArgs& A, const u64* x0, u64 xstride, u64* out0, u
     const u64 N = 1ull << log_n;
     const u32 b2 = 2 * batch;
     Scratch sp, sq;
-    RCCHK(sp.alloc((size_t)b2 * A.size_p * N * 8, s));
-    RCCHK(sq.alloc((size_t)b2 * A.size_q * N * 8, s));
+    RCCHK(sp.alloc((size_t)b2 * A.size_p * N * 8, s, A.plan_q->ctx));
+    RCCHK(sq.alloc((size_t)b2 * A.size_q * N * 8, s, A.plan_q->ctx));
     const u64 ps = A.size_p * N, qs = A.size_q * N;
     RCCHK(plan_ntt_range(A.plan_p, true, A.p0, A.size_p, x0 + qs, sp.w(), xstride, ps, b2, s));
     if (A.tinv_p) RCCHK(scale_towers(A.tinv_p, sp.w(), sp.w(), ps, ps, b2, A.size_p, log_n, s));
@@ -225,8 +228,10 @@ int ofhe_hip_approx_mod_down(ofhe_plan_t pq, ofhe_plan_t pp, ofhe_bconv_t bc, co
     hipStream_t s = pick(stream);
     const u32 Q = pq->towers, P = pp->towers;
     // Tables cached per (t, P^-1 mod q) in the converter: the first call with
-    // a key uploads into freshly allocated memory (no launch reads it yet, so
-    // the blocking copy cannot race); later calls only look the table up.
+    // a key uploads into freshly allocated memory that no launch has read yet
+    // and waits for the copy to land (upload_blocking), so the kernels below,
+    // on whatever stream, read complete tables; later calls only look the
+    // table up and never synchronise.
     std::vector<u64> key(p_inv_modq, p_inv_modq + Q);
     key.push_back(t);
     u64* dtab = nullptr;
@@ -244,7 +249,7 @@ int ofhe_hip_approx_mod_down(ofhe_plan_t pq, ofhe_plan_t pp, ofhe_bconv_t bc, co
             }
             const size_t words = tab.size() * 3;
             HIPCHK(hipMalloc(&dtab, words * sizeof(u64)));
-            hipError_t e = hipMemcpy(dtab, tab.data(), words * sizeof(u64), hipMemcpyHostToDevice);
+            hipError_t e = upload_blocking(dtab, tab.data(), words * sizeof(u64));
             if (e != hipSuccess) {
                 (void)hipFree(dtab);
                 return fail(OFHE_ERR_HIP, std::string("mod-down tables: ") + hipGetErrorString(e));
@@ -431,9 +436,9 @@ static int level_get(ofhe_ks_t k, u32 size_ql, KsLevel** out) {
         hipError_t e = hipSetDevice(k->ctx->device);
         if (e == hipSuccess) e = hipMalloc(&L->d_tow, sizeof(KsTower) * tow.size());
         if (e == hipSuccess) e = hipMalloc(&L->d_pinv, sizeof(TowerScalar) * pinv.size());
-        if (e == hipSuccess) e = hipMemcpy(L->d_tow, tow.data(), sizeof(KsTower) * tow.size(), hipMemcpyHostToDevice);
+        if (e == hipSuccess) e = upload_blocking(L->d_tow, tow.data(), sizeof(KsTower) * tow.size());
         if (e == hipSuccess)
-            e = hipMemcpy(L->d_pinv, pinv.data(), sizeof(TowerScalar) * pinv.size(), hipMemcpyHostToDevice);
+            e = upload_blocking(L->d_pinv, pinv.data(), sizeof(TowerScalar) * pinv.size());
         if (e != hipSuccess) rc = fail(OFHE_ERR_HIP, std::string("level upload: ") + hipGetErrorString(e));
     }
     if (rc != OFHE_OK) {
@@ -458,7 +463,7 @@ static int level_t_tables(ofhe_ks_t k, KsLevel* L, u64 t, const TowerScalar** ou
     for (u32 i = 0; i < l; i++) tab[P + i] = scalar_of(k->q[i], t);
     TowerScalar* d = nullptr;
     HIPCHK(hipMalloc(&d, sizeof(TowerScalar) * tab.size()));
-    hipError_t e = hipMemcpy(d, tab.data(), sizeof(TowerScalar) * tab.size(), hipMemcpyHostToDevice);
+    hipError_t e = upload_blocking(d, tab.data(), sizeof(TowerScalar) * tab.size());
     if (e != hipSuccess) {
         (void)hipFree(d);
         return fail(OFHE_ERR_HIP, std::string("t tables: ") + hipGetErrorString(e));
@@ -635,8 +640,8 @@ int ofhe_hip_ks_core(ofhe_ks_t k, uint32_t size_ql, const uint64_t* c, const uin
     hipStream_t s = pick(stream);
     const u64 N = 1ull << k->log_n, poly = (u64)(size_ql + k->size_p) * N;
     Scratch dg, ct;
-    RCCHK(dg.alloc((size_t)batch * L->beta * poly * 8, s));
-    RCCHK(ct.alloc((size_t)2 * batch * poly * 8, s));
+    RCCHK(dg.alloc((size_t)batch * L->beta * poly * 8, s, k->ctx));
+    RCCHK(ct.alloc((size_t)2 * batch * poly * 8, s, k->ctx));
     u64* c0 = ct.w();
     u64* c1 = ct.w() + (u64)batch * poly;
     // the inner product reads each digit's own towers straight from c (beta <= 4),
@@ -713,7 +718,7 @@ static int plan_table(ofhe_plan_t p, const std::vector<u64>& words, const u64** 
     }
     u64* d = nullptr;
     HIPCHK(hipMalloc(&d, words.size() * sizeof(u64)));
-    hipError_t e = hipMemcpy(d, words.data(), words.size() * sizeof(u64), hipMemcpyHostToDevice);
+    hipError_t e = upload_blocking(d, words.data(), words.size() * sizeof(u64));
     if (e != hipSuccess) {
         (void)hipFree(d);
         return fail(OFHE_ERR_HIP, std::string("rescale tables: ") + hipGetErrorString(e));
@@ -733,6 +738,15 @@ static int rescale_check(ofhe_plan_t p, u32 towers, const u64* x, u64 xs, const 
     if (xs < towers * N || os < (towers - 1) * N) return fail(OFHE_ERR_ARG, "batch stride smaller than the towers");
     if (((xs | os) & 1) || (((uintptr_t)x | (uintptr_t)out) & 15))
         return fail(OFHE_ERR_ARG, "strides must be even and buffers 16-byte aligned");
+    // In place only with equal strides: every launch then reads and writes a
+    // word at the same address from the same thread.  With a packed output
+    // (out_stride = (towers-1)N < x_stride) entry b's output would overwrite
+    // towers of entry b-1's input that other workgroups still read.
+    const u64 x_end = (u64)(uintptr_t)x + 8 * ((u64)(batch - 1) * xs + (u64)towers * N);
+    const u64 o_end = (u64)(uintptr_t)out + 8 * ((u64)(batch - 1) * os + (u64)(towers - 1) * N);
+    const bool overlap = (u64)(uintptr_t)x < o_end && (u64)(uintptr_t)out < x_end;
+    if (overlap && !((const u64*)x == out && xs == os))
+        return fail(OFHE_ERR_ARG, "out overlaps x: in place needs out == x and out_stride == x_stride");
     return OFHE_OK;
 }
 
@@ -776,8 +790,8 @@ static int rescale_run(ofhe_plan_t p, u32 towers, const u64* x, u64 xs, u64* out
         return OFHE_OK;
     }
     Scratch sl, sy;
-    RCCHK(sl.alloc((size_t)batch * N * 8, s));
-    RCCHK(sy.alloc((size_t)batch * L * N * 8, s));
+    RCCHK(sl.alloc((size_t)batch * N * 8, s, p->ctx));
+    RCCHK(sy.alloc((size_t)batch * L * N * 8, s, p->ctx));
     RCCHK(plan_ntt_range(p, true, L, 1, x + (u64)L * N, sl.w(), xs, N, batch, s));
     const u64 ys = (u64)L * N;
     if (log_n > 12 && (!p->split8 || log_n == 16) && OFHE_RESCALE_FUSE) {
@@ -864,11 +878,12 @@ int ofhe_hip_bv_precompute(ofhe_plan_t p, uint32_t towers, const uint64_t* c, ui
     const u64* dsw = nullptr;
     RCCHK(plan_table(p, sw, &dsw));
     Scratch sc;  // c in coefficient form
-    RCCHK(sc.alloc((size_t)batch * TN * 8, s));
+    RCCHK(sc.alloc((size_t)batch * TN * 8, s, p->ctx));
     RCCHK(plan_ntt_range(p, true, 0, T, c, sc.w(), TN, TN, batch, s));
     const u64 dstride = (u64)T * TN;  // words per batch entry of digits
     const bool fused = log_n > 12 && (!p->split8 || log_n == 16) && OFHE_RESCALE_FUSE;
     const u32 bpr = (u32)((N / 2 + 255) / 256);
+    if ((u64)bpr * batch * T >= (1ull << 31)) return fail(OFHE_ERR_ARG, "batch too large for one launch");
     for (u32 i = 0; i < T; i++) {
         u64* di = digits + (u64)i * TN;
         if (fused) {

@@ -52,21 +52,38 @@ int ofhe_hip_init(int device, ofhe_ctx_t* ctx) {
     HIPCHK(hipGetDeviceCount(&n));
     if (device < 0 || device >= n) return fail(OFHE_ERR_ARG, "device index out of range");
     HIPCHK(hipSetDevice(device));
-    // Stream-ordered scratch (hipMallocAsync: ApproxModDown, key switching,
-    // rescaling) stays in the device's default pool across synchronisations
-    // instead of going back to the driver at every sync and being mapped again
-    // by the next call (a rescale timed call by call: 0.79 -> see DESIGN.md).
-    {
-        hipMemPool_t pool = nullptr;
-        if (hipDeviceGetDefaultMemPool(&pool, device) == hipSuccess && pool) {
-            uint64_t keep = UINT64_MAX;
-            (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep);
-        }
-    }
     ofhe_ctx_s* c = new (std::nothrow) ofhe_ctx_s();
     if (!c) return fail(OFHE_ERR_NOMEM, "context allocation failed");
     c->device = device;
+    // Stream-ordered scratch (ApproxModDown, key switching, rescaling) and
+    // ofhe_hip_alloc_async come from a pool of this context's own, which keeps
+    // freed blocks across synchronisations instead of returning them to the
+    // driver at every sync and mapping them again on the next call (a rescale
+    // timed call by call: 0.79 -> 0.62 ms).  The device's default
+    // pool, which other libraries in the process share, is left alone;
+    // ofhe_hip_trim / ofhe_hip_finalize give the memory back.
+    {
+        hipMemPoolProps props = {};
+        props.allocType = hipMemAllocationTypePinned;
+        props.handleTypes = hipMemHandleTypeNone;
+        props.location.type = hipMemLocationTypeDevice;
+        props.location.id = device;
+        hipMemPool_t pool = nullptr;
+        if (hipMemPoolCreate(&pool, &props) == hipSuccess && pool) {
+            uint64_t keep = UINT64_MAX;
+            (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep);
+            c->pool = pool;
+        }
+    }
     *ctx = c;
+    return OFHE_OK;
+}
+
+int ofhe_hip_trim(ofhe_ctx_t ctx, size_t keep_bytes) {
+    if (!ctx) return fail(OFHE_ERR_ARG, "ctx is NULL");
+    if (!ctx->pool) return OFHE_OK;
+    HIPCHK(hipSetDevice(ctx->device));
+    HIPCHK(hipMemPoolTrimTo(ctx->pool, keep_bytes));
     return OFHE_OK;
 }
 
@@ -75,6 +92,7 @@ int ofhe_hip_finalize(ofhe_ctx_t ctx) {
     if (ctx->live.exchange(0) == 0) return fail(OFHE_ERR_STATE, "context already finalized");
     (void)hipSetDevice(ctx->device);
     (void)hipDeviceSynchronize();
+    if (ctx->pool) (void)hipMemPoolDestroy(ctx->pool);  // blocks still allocated from it are released with it
     delete ctx;
     return OFHE_OK;
 }
@@ -98,7 +116,8 @@ int ofhe_hip_free(ofhe_ctx_t ctx, void* dptr) {
 int ofhe_hip_alloc_async(ofhe_ctx_t ctx, size_t bytes, void** dptr, void* stream) {
     if (!ctx || !dptr) return fail(OFHE_ERR_ARG, "NULL argument");
     HIPCHK(hipSetDevice(ctx->device));
-    hipError_t e = hipMallocAsync(dptr, bytes ? bytes : 1, pick(stream));
+    hipError_t e = ctx->pool ? hipMallocFromPoolAsync(dptr, bytes ? bytes : 1, ctx->pool, pick(stream))
+                             : hipMallocAsync(dptr, bytes ? bytes : 1, pick(stream));
     if (e != hipSuccess) return fail(OFHE_ERR_NOMEM, std::string("hipMallocAsync: ") + hipGetErrorString(e));
     return OFHE_OK;
 }
@@ -317,16 +336,16 @@ int ofhe_hip_plan_create(ofhe_ctx_t ctx, uint32_t log_n, uint32_t towers, const 
     if (e == hipSuccess) e = hipMalloc(&p->d_itw, sizeof(u64) * 2 * TN);
     if (e == hipSuccess) e = hipMalloc(&p->d_tw3, sizeof(u64) * (tw3.size() ? tw3.size() : 2));
     if (e == hipSuccess && tw3.size())
-        e = hipMemcpy(p->d_tw3, tw3.data(), sizeof(u64) * tw3.size(), hipMemcpyHostToDevice);
+        e = upload_blocking(p->d_tw3, tw3.data(), sizeof(u64) * tw3.size());
     if (e == hipSuccess) e = hipMalloc(&p->d_dtw, sizeof(u64) * 2 * TN);
     if (e == hipSuccess) e = hipMalloc(&p->d_twist, sizeof(u64) * 2 * TN);
     if (e == hipSuccess) e = hipMalloc(&p->d_twist_r, sizeof(u64) * 2 * TN);
-    if (e == hipSuccess) e = hipMemcpy(p->d_dtw, dtw.data(), sizeof(u64) * 2 * TN, hipMemcpyHostToDevice);
-    if (e == hipSuccess) e = hipMemcpy(p->d_twist, twist.data(), sizeof(u64) * 2 * TN, hipMemcpyHostToDevice);
-    if (e == hipSuccess) e = hipMemcpy(p->d_twist_r, twist_r.data(), sizeof(u64) * 2 * TN, hipMemcpyHostToDevice);
-    if (e == hipSuccess) e = hipMemcpy(p->d_tc, tc.data(), sizeof(TowerConst) * towers, hipMemcpyHostToDevice);
-    if (e == hipSuccess) e = hipMemcpy(p->d_tw, tw.data(), sizeof(u64) * 2 * TN, hipMemcpyHostToDevice);
-    if (e == hipSuccess) e = hipMemcpy(p->d_itw, itw.data(), sizeof(u64) * 2 * TN, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = upload_blocking(p->d_dtw, dtw.data(), sizeof(u64) * 2 * TN);
+    if (e == hipSuccess) e = upload_blocking(p->d_twist, twist.data(), sizeof(u64) * 2 * TN);
+    if (e == hipSuccess) e = upload_blocking(p->d_twist_r, twist_r.data(), sizeof(u64) * 2 * TN);
+    if (e == hipSuccess) e = upload_blocking(p->d_tc, tc.data(), sizeof(TowerConst) * towers);
+    if (e == hipSuccess) e = upload_blocking(p->d_tw, tw.data(), sizeof(u64) * 2 * TN);
+    if (e == hipSuccess) e = upload_blocking(p->d_itw, itw.data(), sizeof(u64) * 2 * TN);
     if (e != hipSuccess) {
         ofhe_hip_plan_destroy(p);
         return fail(OFHE_ERR_HIP, std::string("plan upload: ") + hipGetErrorString(e));
@@ -796,7 +815,7 @@ static bool nm_ready(ofhe_plan_t p) {
     }
     void* d = nullptr;
     if (hipMalloc(&d, tab.size()) != hipSuccess) return false;
-    if (hipMemcpy(d, tab.data(), tab.size(), hipMemcpyHostToDevice) != hipSuccess) {
+    if (upload_blocking(d, tab.data(), tab.size()) != hipSuccess) {
         (void)hipFree(d);
         return false;
     }
@@ -1153,7 +1172,7 @@ int ofhe_hip_bconv_create(ofhe_ctx_t ctx, uint32_t log_n, uint32_t size_q, uint3
     b->ctx = ctx;
     hipError_t e = hipSetDevice(ctx->device);
     if (e == hipSuccess) e = hipMalloc(&b->d_mem, words_all * sizeof(u64));
-    if (e == hipSuccess) e = hipMemcpy(b->d_mem, h.data(), words_all * sizeof(u64), hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = upload_blocking(b->d_mem, h.data(), words_all * sizeof(u64));
     if (e != hipSuccess) {
         (void)hipFree(b->d_mem);
         delete b;

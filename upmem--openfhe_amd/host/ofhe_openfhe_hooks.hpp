@@ -16,7 +16,7 @@
 // over every tower and scatters back (the host-buffer integration; the
 // resident integration keeps DCRTPolyHip objects instead, ofhe_dcrt.hpp).
 //
-//   DCRTPolyImpl::SwitchFormat          dcrtpoly-impl.h:2518-2524 -> SwitchFormat(m_vectors, m_format == COEFFICIENT)
+//   DCRTPolyImpl::SwitchFormat          dcrtpoly-impl.h:2516-2523 -> if (!SwitchFormat(m_vectors)) <reference loop>
 //   DCRTPolyImpl::operator*= / Times    dcrtpoly.h:142-148, 185-200 -> TimesEq(m_vectors, rhs.m_vectors)
 //   DCRTPolyImpl::operator+= / -=       dcrtpoly-impl.h:410-416     -> PlusEq / MinusEq
 //   DCRTPolyImpl::ApproxSwitchCRTBasis  dcrtpoly-impl.h:1034-1063   -> ApproxSwitchCRTBasis(...)
@@ -25,6 +25,7 @@
 #include <cstdint>
 #include <map>
 #include <memory>
+#include <type_traits>
 #include <utility>
 #include <vector>
 
@@ -78,11 +79,38 @@ inline Staging& staging(int device, size_t words, int slot = 0) {
     return *s;
 }
 
-// DCRTPolyImpl::SwitchFormat (dcrtpoly-impl.h:2518-2524): to_eval = true is
-// COEFFICIENT -> EVALUATION (ForwardTransformToBitReverseInPlace per tower),
-// false the inverse.  The caller flips m_format as the reference does.
+// Rings below this stay on the reference's CPU loop: binfhe's rings (N <= 2^11,
+// rgsw-acc-*.cpp) are launch-latency bound on the GPU and PCIe-bound through
+// the host-buffer hooks.
+constexpr uint32_t kDeviceMinRing = 4096;
+
+// Whether the device takes DCRTPolyImpl::SwitchFormat for these towers: a
+// power-of-two cyclotomic (PolyImpl::SwitchFormat sends rd != co / 2 to
+// ArbitrarySwitchFormat, poly-impl.h:412-420), ring dimension >= kDeviceMinRing,
+// every tower in the same format.
 template <class Towers>
-void SwitchFormat(Towers& towers, bool to_eval, int device = 0) {
+bool device_switch_format(const Towers& towers) {
+    if (towers.empty()) return false;
+    const auto& p0 = *towers[0].GetParams();
+    const uint32_t n = (uint32_t)p0.GetRingDimension();
+    if (n < kDeviceMinRing || (uint64_t)p0.GetCyclotomicOrder() != 2 * (uint64_t)n) return false;
+    for (const auto& t : towers)
+        if (t.GetFormat() != towers[0].GetFormat()) return false;
+    return true;
+}
+
+// DCRTPolyImpl::SwitchFormat (dcrtpoly-impl.h:2516-2523): every tower
+// COEFFICIENT -> EVALUATION (ForwardTransformToBitReverseInPlace) or back
+// (InverseTransformFromBitReverseInPlace) in one launch, then each tower's
+// format flipped with PolyImpl::OverrideFormat (poly.h:179), as
+// PolyImpl::SwitchFormat does per tower (poly-impl.h:412-432).  Returns false,
+// touching nothing, when device_switch_format() says no: the caller then runs
+// the reference's own per-tower loop.
+template <class Towers>
+bool SwitchFormat(Towers& towers, int device = 0) {
+    if (!device_switch_format(towers)) return false;
+    using Fmt = std::decay_t<decltype(towers[0].GetFormat())>;
+    const bool to_eval = towers[0].GetFormat() == Fmt::COEFFICIENT;
     TowerView v = view(towers);
     auto plan = PlanCache::get(device, v.log_n, v.q, v.psi);
     const size_t words = v.q.size() * (size_t)v.n;
@@ -94,6 +122,8 @@ void SwitchFormat(Towers& towers, bool to_eval, int device = 0) {
           "hooks::SwitchFormat");
     st.download(words);
     st.scatter(v.data, v.n);
+    for (auto& t : towers) t.OverrideFormat(to_eval ? Fmt::EVALUATION : Fmt::COEFFICIENT);
+    return true;
 }
 
 namespace detail {

@@ -60,6 +60,7 @@ _SIGS = {
     "ofhe_hip_copy_to_host": (ctypes.c_int, [_vp, _vp, _vp, ctypes.c_size_t, _vp]),
     "ofhe_hip_copy_device": (ctypes.c_int, [_vp, _vp, _vp, ctypes.c_size_t, _vp]),
     "ofhe_hip_sync": (ctypes.c_int, [_vp, _vp]),
+    "ofhe_hip_trim": (ctypes.c_int, [_vp, ctypes.c_size_t]),
     "ofhe_hip_plan_create": (ctypes.c_int, [_vp, ctypes.c_uint32, ctypes.c_uint32, _u64p, _u64p,
                                             ctypes.POINTER(_vp)]),
     "ofhe_hip_plan_destroy": (ctypes.c_int, [_vp]),
@@ -225,6 +226,10 @@ class Context:
     def sync(self, stream: int = 0) -> None:
         _check(lib().ofhe_hip_sync(self.handle, _vp(stream or None)))
 
+    def trim(self, keep_bytes: int = 0) -> None:
+        """Give the context's cached stream-ordered memory back to the device."""
+        _check(lib().ofhe_hip_trim(self.handle, keep_bytes))
+
 
 class NTTPlan:
     """Device-resident NTT tables for N = 2**log_n and one modulus per tower.
@@ -345,7 +350,7 @@ class NTTPlan:
     # --- rescaling (DCRTPolyImpl::DropLastElementAndScale / ModReduce) ---
     def drop_last_and_scale(self, towers: int, x: int, x_stride: int, out: int, out_stride: int, eval_form: bool,
                             ql_ql_inv_modql_divql_modq, ql_inv_modq, batch: int = 1, stream: int = 0) -> None:
-        """dcrtpoly-impl.h:746-768 on [batch][towers] -> [batch][towers - 1] (out may alias x)."""
+        """dcrtpoly-impl.h:746-768 on [batch][towers] -> [batch][towers - 1] (out may be x with equal strides; other overlap is rejected)."""
         c, a = list(ql_ql_inv_modql_divql_modq), list(ql_inv_modq)
         if len(c) < towers - 1 or len(a) < towers - 1:
             raise MathError("need towers - 1 constants")
@@ -355,7 +360,7 @@ class NTTPlan:
 
     def mod_reduce(self, towers: int, x: int, x_stride: int, out: int, out_stride: int, eval_form: bool, t: int,
                    neg_t_inv_modq: int, ql_inv_modq, batch: int = 1, stream: int = 0) -> None:
-        """dcrtpoly-impl.h:792-812 on [batch][towers] -> [batch][towers - 1] (out may alias x)."""
+        """dcrtpoly-impl.h:792-812 on [batch][towers] -> [batch][towers - 1] (out may be x with equal strides; other overlap is rejected)."""
         a = list(ql_inv_modq)
         if len(a) < towers - 1:
             raise MathError("need towers - 1 constants")

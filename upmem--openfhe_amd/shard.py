@@ -60,8 +60,18 @@ def open_comm(ctx, rank: int, world: int):
 
     import ofhe_hip as H
 
-    uid = [H.comm_unique_id() if rank == 0 else None]
+    # rank 0 always broadcasts: the id, or the reason it has none, so a failed
+    # ofhe_hip_comm_unique_id never leaves the peers waiting in this broadcast
+    # while rank 0 has moved on to the next collective
+    uid = [None]
+    if rank == 0:
+        try:
+            uid[0] = H.comm_unique_id()
+        except Exception as e:  # noqa: BLE001  (library missing or RCCL refused: fall back, never hang)
+            uid[0] = "unique id failed on rank 0: " + str(e)
     dist.broadcast_object_list(uid, src=0)
+    if isinstance(uid[0], str):
+        raise H.MathError(uid[0])
     return H.Comm(ctx, world, rank, uid[0])
 
 
@@ -106,8 +116,10 @@ def key_broadcaster(ctx, rank: int, world: int):
 
     comm, err = None, None
     try:
+        if ctx is None:
+            raise H.MathError("no device context (CPU rehearsal)")
         comm = open_comm(ctx, rank, world)
-    except H.MathError as e:
+    except Exception as e:  # noqa: BLE001
         err = str(e)
     backend = dist.get_backend()
     dev = torch.device("cuda", torch.cuda.current_device()) if backend == "nccl" else torch.device("cpu")
