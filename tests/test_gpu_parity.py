@@ -439,3 +439,36 @@ def test_block_mma_vs_oracle(hip, O, monkeypatch, batch, edge):
     assert np.array_equal(outs[0], outs[1])
     sel = slice(None) if batch <= 17 else [0, 127, 128, batch - 1]
     assert np.array_equal(outs[0][sel], O.ntt_mul_intt(a[sel], b[sel], tb))
+
+
+@pytest.mark.parametrize("T,batch,edge", [(2, 1, False), (3, 5, False), (16, 2, False), (2, 3, True)])
+def test_block_m16_vs_oracle(hip, O, monkeypatch, T, batch, edge):
+    """N = 2^16 fused pipeline with the four-round matrix-core block pass
+    (k_block_m16, csrc/ntt_m16.hpp: twist, shared-F rounds, explicit twiddles)
+    equals the oracle and the butterfly block pass bit for bit; edge =
+    all-(q-1) inputs.  Opt-in at plan creation (OFHE_BLOCK_M16=1)."""
+    import torch
+
+    H, ctx = hip
+    log_n = 16
+    n = 1 << log_n
+    qs, rs = O.moduli_chain(log_n, T)
+    tb = O.Tables(n, qs, rs)
+    if edge:
+        a = np.broadcast_to(np.array(qs, np.uint64)[None, :, None] - np.uint64(1), (batch, T, n)).copy()
+        b = a.copy()
+    else:
+        a = O.uniform_dcrt(batch, T, n, qs, 700 + batch)
+        b = O.uniform_dcrt(batch, T, n, qs, 800 + batch)
+    outs = []
+    for env in ("1", "0"):
+        monkeypatch.setenv("OFHE_BLOCK_M16", env)
+        plan = H.NTTPlan(ctx, log_n, qs, rs)
+        xa, xb = dev(a), dev(b)
+        xc = torch.empty_like(xa)
+        plan.ntt_mul_intt(xa.data_ptr(), xb.data_ptr(), xc.data_ptr(), batch, stream())
+        outs.append(host(xc))
+        plan.close()
+    assert np.array_equal(outs[1], O.ntt_mul_intt(a, b, tb))
+    bad = np.argwhere(outs[0] != outs[1])
+    assert bad.size == 0, (len(bad), bad[:5].tolist())

@@ -30,6 +30,24 @@ untracked build output) and writes the variants:
             blocks executed under EXEC = 0
   vnop      s_nop 1 after every VALU instruction (two wait states between any
             VALU result and its next reader)
+  rcpnop    s_nop 4 after the one transcendental instruction (v_rcp_iflag_f32,
+            the reciprocal of `towers` for row % towers), before its consumer
+  allnop    s_nop 4 after EVERY instruction of the kernel (five wait states
+            everywhere: no intra-wave pipeline hazard survives this)
+  nont      the loads and stores without the non-temporal hint (`off nt` ->
+            `off`)
+  vmwait    s_waitcnt vmcnt(0) after every global load (each load completes
+            before the next instruction issues)
+  dump      out0's store replaced by the lane's tower constants as the kernel
+            holds them at the end: q (v[24:25]) in word 2i, nshift (v51) in
+            the low half of word 2i + 1 -- checked against the table per
+            element, next to that element's out2
+  vgpr64    the unchanged code with its VGPR allocation raised from 56 to 64
+            (next_free_vgpr / accum_offset / metadata only)
+  vgpr48x   every wave's allocation 56 -> 72 (above 64: 7 waves per SIMD)
+  dumpin    out0 receives the c1 pair as loaded (v[14:17], stored right after
+            the first s_waitcnt that covers its load, through v[56:57]) and
+            keeps nothing else: the kernel's own view of its inputs
 
   python tools/diag/t2asm_build.py [path/to/ofhe_hip.s]
 """
@@ -88,6 +106,30 @@ def variant(text, kind):
         return text
     if kind == "nobranch":
         return nobranch(text)
+    if kind == "nont":
+        return text.replace(", off nt", ", off")
+    if kind in ("vgpr64", "vgpr48x"):
+        n = 64 if kind == "vgpr64" else 72
+        text = text.replace(".amdhsa_next_free_vgpr 56", ".amdhsa_next_free_vgpr %d" % n)
+        text = text.replace(".amdhsa_accum_offset 56", ".amdhsa_accum_offset %d" % n)
+        return re.sub(r"(\.vgpr_count:\s+)56", r"\g<1>%d" % n, text)
+    if kind == "dumpin":
+        old = "\tglobal_store_dwordx4 v[2:3], v[6:9], off nt"
+        assert text.count(old) == 1
+        text = text.replace(old, "")
+        w = "\ts_waitcnt vmcnt(5)"
+        assert text.count(w) == 1
+        text = text.replace(w, w + "\n\tv_lshl_add_u64 v[56:57], s[12:13], 0, v[20:21]\n"
+                                   "\tglobal_store_dwordx4 v[56:57], v[14:17], off")
+        text = text.replace(".amdhsa_next_free_vgpr 56", ".amdhsa_next_free_vgpr 58")
+        text = text.replace(".amdhsa_accum_offset 56", ".amdhsa_accum_offset 60")
+        text = re.sub(r"(\.vgpr_count:\s+)56", r"\g<1>58", text)
+        return text
+    if kind == "dump":
+        old = "\tglobal_store_dwordx4 v[2:3], v[6:9], off nt"
+        assert text.count(old) == 1
+        return text.replace(old, "\tglobal_store_dwordx2 v[2:3], v[24:25], off\n"
+                                 "\tglobal_store_dword v[2:3], v51, off offset:8")
     out = []
     lines = text.split("\n")
     for i, l in enumerate(lines):
@@ -110,6 +152,12 @@ def variant(text, kind):
             out.append("\ts_nop 4")
         if kind == "vnop" and s.startswith("v_"):
             out.append("\ts_nop 1")
+        if kind == "rcpnop" and s.startswith("v_rcp_iflag_f32"):
+            out.append("\ts_nop 4")
+        if kind == "allnop" and re.match(r"^[vs]_", s) and not s.startswith(("s_endpgm", "s_cbranch", "s_branch")):
+            out.append("\ts_nop 4")
+        if kind == "vmwait" and s.startswith("global_load"):
+            out.append("\ts_waitcnt vmcnt(0)")
     return "\n".join(out)
 
 
@@ -119,7 +167,7 @@ def main():
     if src:
         open(orig, "w").write(extract(src))
     text = open(orig).read()
-    for kind in ("orig", "nop", "carry", "endwait", "zero", "execnop", "nobranch", "vnop"):
+    for kind in ("orig", "nop", "carry", "endwait", "zero", "execnop", "nobranch", "vnop", "rcpnop", "allnop", "nont", "vmwait", "dump", "dumpin", "vgpr64", "vgpr48x"):
         s = os.path.join(HERE, f"t2_{kind}_gen.s")
         o = os.path.join(HERE, f"t2_{kind}.o")
         co = os.path.join(HERE, f"t2_{kind}.hsaco")

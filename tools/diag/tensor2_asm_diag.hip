@@ -12,6 +12,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 typedef unsigned long long u64;
@@ -105,6 +106,71 @@ static long run(hipFunction_t fn, const char* name, u32 log_n, u32 towers, u32 b
                     }
                 }
         }
+        if (!strcmp(name, "dump")) {
+            // out0 holds (q, nshift) as the lane had them; out2 as computed
+            long cbad = 0, both = 0, o2bad = 0, shownd = 0;
+            for (u64 i = 0; i < npairs; i++) {
+                const u64 e = 2 * i;
+                const u32 t = (u32)((e >> log_n) % towers);
+                const bool cb = o[0][e] != tc[t].q || (u32)o[0][e + 1] != tc[t].nshift;
+                const bool b2 = o[2][e] != mulmod(h[1][e], h[3][e], tc[t].q) ||
+                                o[2][e + 1] != mulmod(h[1][e + 1], h[3][e + 1], tc[t].q);
+                cbad += cb;
+                o2bad += b2;
+                both += cb && b2;
+                if (cb && shownd++ < 4)
+                    printf("    pair %llu (t=%u): held q=%llx nshift=%u, table q=%llx nshift=%u\n", i, t, o[0][e],
+                           (u32)o[0][e + 1], tc[t].q, tc[t].nshift);
+            }
+            printf("    pairs with wrong constants %ld, with a wrong out2 %ld, both %ld (of %llu)\n", cbad, o2bad, both,
+                   npairs);
+        }
+        if (!strcmp(name, "dumpin")) {
+            long ibad = 0, both = 0, o2bad = 0, showni = 0;
+            for (u64 i = 0; i < npairs; i++) {
+                const u64 e = 2 * i;
+                const u32 t = (u32)((e >> log_n) % towers);
+                const bool ib = o[0][e] != h[1][e] || o[0][e + 1] != h[1][e + 1];
+                const bool b2 = o[2][e] != mulmod(h[1][e], h[3][e], tc[t].q) ||
+                                o[2][e + 1] != mulmod(h[1][e + 1], h[3][e + 1], tc[t].q);
+                ibad += ib;
+                o2bad += b2;
+                both += ib && b2;
+                if (ib && showni++ < 4)
+                    printf("    pair %llu: loaded c1 %llx %llx, memory holds %llx %llx\n", i, o[0][e], o[0][e + 1],
+                           h[1][e], h[1][e + 1]);
+            }
+            printf("    pairs whose c1 load differs from memory %ld, with a wrong out2 %ld, both %ld (of %llu)\n", ibad,
+                   o2bad, both, npairs);
+        }
+        if (tot && rep == 0 && getenv("T2_MATCH")) {
+            // is a wrong word some other element's correct result?
+            std::unordered_map<u64, u64> where;
+            for (u64 e = 0; e < words; e++) {
+                const u32 t = (u32)((e >> log_n) % towers);
+                const u64 q = tc[t].q;
+                where[mulmod(h[1][e], h[3][e], q)] = e * 4 + 2;
+                where[mulmod(h[2][e], h[0][e], q)] = e * 4 + 0;
+                where[(mulmod(h[1][e], h[2][e], q) + mulmod(h[0][e], h[3][e], q)) % q] = e * 4 + 1;
+                where[mulmod(h[1][e], h[2][e], q)] = e * 4 + 3;  // c1 d0 alone
+            }
+            long found = 0, shownm = 0, checked = 0;
+            for (u64 e = 0; e < words && checked < 20000; e++) {
+                const u32 t = (u32)((e >> log_n) % towers);
+                const u64 q = tc[t].q;
+                const u64 w2 = mulmod(h[1][e], h[3][e], q);
+                if (o[2][e] == w2) continue;
+                checked++;
+                auto it = where.find(o[2][e]);
+                if (it != where.end()) {
+                    found++;
+                    if (shownm++ < 8)
+                        printf("    out2[%llu] = result %llu of element %llu (delta %lld)\n", e, it->second & 3,
+                               it->second >> 2, (long long)(it->second >> 2) - (long long)e);
+                }
+            }
+            printf("    %ld of %ld wrong out2 words are another element's correct result\n", found, checked);
+        }
         if (tot > worst) worst = tot;
         printf("%-7s log_n=%u towers=%u batch=%u grid=%llu x %u lds=%u rep=%d bad=%ld per (tower,out):", name, log_n,
                towers, batch, blocks, bdim, lds, rep, tot);
@@ -121,7 +187,8 @@ static long run(hipFunction_t fn, const char* name, u32 log_n, u32 towers, u32 b
 int main(int argc, char** argv) {
     const std::string dir = argc > 1 ? argv[1] : ".";
     const char* kname = "_ZN4ofhe9k_tensor2ILi0EEEvPKNS_10TowerConstEPKmS5_S5_S5_PmS6_S6_mjj";
-    const char* kinds[] = {"orig", "nobranch", "vnop", "endwait", "zero", "execnop", "nop", "carry"};
+    const char* kinds[] = {"vgpr64", "vgpr48x", "orig", "dumpin", "dump", "allnop", "nont", "vmwait", "rcpnop", "nobranch", "vnop", "endwait", "zero",
+                           "execnop", "nop", "carry"};
     const int only = getenv("T2_ONLY") ? atoi(getenv("T2_ONLY")) : 99;
     const int nk = only < 99 ? only : (int)(sizeof(kinds) / sizeof(kinds[0]));
     long bad[16] = {};

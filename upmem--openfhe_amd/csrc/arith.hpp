@@ -28,6 +28,15 @@ namespace ofhe {
 typedef uint64_t u64;
 typedef uint32_t u32;
 
+// VGPR allocation floor for every kernel of the library.  Round 2's
+// grid-stride EvalMultCore, compiled to 56 VGPRs, returned wrong words
+// whenever two or more of its workgroups shared a CU; the SAME machine code
+// with its allocation raised to 64 (or 72) VGPRs is exact at every shape
+// (tools/diag, DESIGN.md "The round-2 EvalMultCore failure").  A clobber of
+// v63 makes every kernel allocate at least 64 VGPRs; at 64 a SIMD still holds
+// its maximum of 8 waves, so occupancy is unchanged.
+#define OFHE_VGPR_FLOOR() asm volatile("" ::: "v63")
+
 __device__ __forceinline__ u32 lo32(u64 x) { return (u32)x; }
 __device__ __forceinline__ u32 hi32(u64 x) { return (u32)(x >> 32); }
 __device__ __forceinline__ u64 pack(u32 lo, u32 hi) { return ((u64)hi << 32) | lo; }

@@ -149,6 +149,7 @@ __device__ __forceinline__ u64 bm_reduce(const int* C, const BmRed& R, const BmW
 template <int KS, bool LAZY, bool SPQ>
 __global__ __launch_bounds__(BCONV_MMA_THREADS, OFHE_BCONV_MMA_WAVES) void k_bconv_mma(
     BconvArgs A, const u64* __restrict__ x, u64* __restrict__ out, u32 batch) {
+    OFHE_VGPR_FLOOR();
     constexpr bool WIDE = KS > 8;
     constexpr bool PF = OFHE_BCONV_MMA_PF && KS <= 8;  // registers: the prefetch holds 2 KS words
     extern __shared__ __attribute__((aligned(16))) unsigned char bm_lds[];

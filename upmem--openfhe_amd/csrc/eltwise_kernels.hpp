@@ -39,6 +39,7 @@ template <int V = 0>  // a template: this header is included by several translat
 __global__ __launch_bounds__(256) void k_tensor2(const TowerConst* __restrict__ tcs, const u64* c0, const u64* c1,
                                                  const u64* d0, const u64* d1, u64* o0, u64* o1, u64* o2, u32 bpr,
                                                  u32 log_n, u32 towers) {
+    OFHE_VGPR_FLOOR();
     const u32 row = blockIdx.x / bpr;
     const u64 j = 2 * ((u64)(blockIdx.x % bpr) * blockDim.x + threadIdx.x);
     if (j >= (1ull << log_n)) return;
@@ -61,6 +62,7 @@ template <int OP>
 __global__ __launch_bounds__(256) void k_eltwise(const TowerConst* __restrict__ tcs,
                                                  const u64* a, const u64* b, u64* c, u64 npairs,
                                                  u32 log_n, u32 towers) {
+    OFHE_VGPR_FLOOR();
     constexpr int ELT_U = elt_unroll(OP);
     const u64 stride = (u64)gridDim.x * blockDim.x;
     for (u64 i0 = (u64)blockIdx.x * blockDim.x + threadIdx.x; i0 < npairs; i0 += stride * ELT_U) {
@@ -111,6 +113,7 @@ struct ScalarPack {
 template <int OP>
 __global__ __launch_bounds__(256) void k_scalar(ScalarPack S, const u64* a, u64* c, u64 npairs, u32 log_n,
                                                 u32 cnt, u32 t0, u32 towers) {
+    OFHE_VGPR_FLOOR();
     const u64 stride = (u64)gridDim.x * blockDim.x;
     const u64 mask = (1ull << log_n) - 1;
     constexpr int ELT_U = elt_unroll(OP);
@@ -154,6 +157,7 @@ __global__ __launch_bounds__(256) void k_scalar(ScalarPack S, const u64* a, u64*
 // range; the other words are the caller's (in place, or copied beforehand).
 static __global__ __launch_bounds__(256) void k_scalar_at(ScalarPack S, const u64* a, u64* c, u32 batch, u32 log_n,
                                                    u32 cnt, u32 t0, u32 towers, u64 idx) {
+    OFHE_VGPR_FLOOR();
     const u64 r = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (r >= (u64)batch * cnt) return;
     const u32 tl = (u32)(r % cnt);
@@ -169,6 +173,7 @@ static __global__ __launch_bounds__(256) void k_scalar_at(ScalarPack S, const u6
 // seed + k * 0x9E3779B97F4A7C15).
 static __global__ __launch_bounds__(256) void k_fill_uniform(const TowerConst* __restrict__ tcs, u64* dst, u64 words,
                                                       u32 log_n, u32 towers, u32 b0, u64 seed) {
+    OFHE_VGPR_FLOOR();
     const u64 stride = (u64)gridDim.x * blockDim.x;
     for (u64 e = (u64)blockIdx.x * blockDim.x + threadIdx.x; e < words; e += stride) {
         const u32 row = (u32)(e >> log_n);
@@ -213,6 +218,7 @@ struct BconvArgs {
 template <int PT>
 __global__ __launch_bounds__(256) void k_bconv(BconvArgs A, const u64* __restrict__ x,
                                                u64* __restrict__ out, u32 batch) {
+    OFHE_VGPR_FLOOR();
     const u32 N = 1u << A.log_n;
     const u64 gid = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (gid >= (u64)batch * N) return;
@@ -305,6 +311,7 @@ __device__ __forceinline__ u64 limb_reduce(u64 a0, u64 a1, u64 a2, u64 a3, const
 template <int PT>
 __global__ __launch_bounds__(256) void k_bconv_limb(BconvArgs A, const u64* __restrict__ x, u64* __restrict__ out,
                                                     u32 batch) {
+    OFHE_VGPR_FLOOR();
     // y limbs of every source tower, computed once per coefficient and kept
     // in this thread's own LDS column across the P tiles (no barrier needed)
     __shared__ u64 ys[BCONV_LIMB_QMAX][256];

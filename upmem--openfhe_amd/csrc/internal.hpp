@@ -146,6 +146,11 @@ struct ofhe_plan_s {
     void* d_nm = nullptr;
     int nm_state = 0;  // 0 not built, 1 ready, -1 not applicable
     std::mutex nm_mu;
+    // k_block_m16 (ntt_m16.hpp): F / F' fragments, reduction constants and
+    // twist / twiddle tables per tower, built on the first fused call
+    void* d_m16 = nullptr;
+    int m16_state = 0;  // 0 not built, 1 ready, -1 not applicable
+    std::mutex m16_mu;
 };
 
 struct ofhe_bconv_s {

@@ -31,6 +31,7 @@ __device__ __forceinline__ PairIndex pair_index(u64 i, u32 log_n, u32 towers) {
 __global__ __launch_bounds__(256) void k_scale_towers(const TowerScalar* __restrict__ ts, const u64* x, u64* out,
                                                       u64 xstride, u64 ostride, u64 npairs, u32 log_n,
                                                       u32 towers) {
+    OFHE_VGPR_FLOOR();
     const u64 step = (u64)gridDim.x * blockDim.x;
     for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < npairs; i += step) {
         const PairIndex p = pair_index(i, log_n, towers);
@@ -47,6 +48,7 @@ __global__ __launch_bounds__(256) void k_scale_towers(const TowerScalar* __restr
 __global__ __launch_bounds__(256) void k_sub_scale(const TowerScalar* __restrict__ ts, const u64* x, const u64* y,
                                                    u64* out, u64 xstride, u64 ystride, u64 ostride, u64 npairs,
                                                    u32 log_n, u32 towers) {
+    OFHE_VGPR_FLOOR();
     const u64 step = (u64)gridDim.x * blockDim.x;
     for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < npairs; i += step) {
         const PairIndex p = pair_index(i, log_n, towers);
@@ -78,6 +80,7 @@ __global__ __launch_bounds__(256) void k_ks_inner(const KsTower* __restrict__ tw
                                                   const u64* __restrict__ kb, const u64* __restrict__ ka,
                                                   u64* __restrict__ ct0, u64* __restrict__ ct1, u64 key_stride,
                                                   u32 beta, u64 npairs, u32 log_n, u32 towers) {
+    OFHE_VGPR_FLOOR();
     const u64 step = (u64)gridDim.x * blockDim.x;
     const u64 poly = (u64)towers << log_n;
     for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < npairs; i += step) {
@@ -169,6 +172,7 @@ __global__ __launch_bounds__(256) void k_ks_inner_bs(const KsTower* __restrict__
                                                      u64* __restrict__ ct0, u64* __restrict__ ct1, u64 key_stride,
                                                      u32 batch, u64 nthreads, u32 log_n, u32 towers,
                                                      const u64* __restrict__ c_in, u64 c_stride, KsOwn own) {
+    OFHE_VGPR_FLOOR();
     const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= nthreads) return;
     const u64 e = C * i;
@@ -234,6 +238,7 @@ __global__ __launch_bounds__(256) void k_ks_inner_bs(const KsTower* __restrict__
 
 // NativeVectorT::SwitchModulus (mubintvecnat.cpp:111-136), value for value.
 __global__ __launch_bounds__(256) void k_switch_modulus(const u64* src, u64* dst, u64 n, u64 om, u64 nm) {
+    OFHE_VGPR_FLOOR();
     const u64 step = (u64)gridDim.x * blockDim.x;
     const u64 half = om >> 1;
     const bool up = nm > om;
@@ -274,6 +279,7 @@ struct SwArgs {
 // skips the multiply
 template <int MODE>
 __global__ __launch_bounds__(256) void k_switch_scale(SwArgs A, u32 bpr) {
+    OFHE_VGPR_FLOOR();
     const u32 row = blockIdx.x / bpr, b = row / A.towers, t = row % A.towers;  // bpr blocks per row
     const u64 N = 1ull << A.log_n;
     const u64 j = 2 * ((u64)(blockIdx.x % bpr) * blockDim.x + threadIdx.x);
@@ -315,6 +321,7 @@ struct BvArgs {
     u32 nd, towers, key_towers, log_n;
 };
 __global__ __launch_bounds__(256) void k_bv_inner(BvArgs A, u32 bpr) {
+    OFHE_VGPR_FLOOR();
     const u32 row = blockIdx.x / bpr, b = row / A.towers, t = row % A.towers;
     const u64 N = 1ull << A.log_n;
     const u64 j = (u64)(blockIdx.x % bpr) * blockDim.x + threadIdx.x;
@@ -349,6 +356,7 @@ __global__ __launch_bounds__(256) void k_bv_inner(BvArgs A, u32 bpr) {
 template <bool EVAL>
 __global__ __launch_bounds__(256) void k_automorphism(const TowerConst* __restrict__ tcs, const u64* src, u64* dst,
                                                       u32 k, u64 total, u32 log_n, u32 towers) {
+    OFHE_VGPR_FLOOR();
     const u64 step = (u64)gridDim.x * blockDim.x;
     const u64 n = 1ull << log_n, mask = n - 1, m2 = 2 * n - 1;
     for (u64 e = (u64)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += step) {

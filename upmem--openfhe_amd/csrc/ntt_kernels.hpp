@@ -527,6 +527,7 @@ __device__ __forceinline__ void wave_stage_out(const u64 (&v)[16], u64* lds, u32
 template <int MODE, bool SPQ, int NR>
 __global__ __launch_bounds__(256, OFHE_KB_WAVES) void k_block(PlanArgs P, const u64* src, u64* dst,
                                                               const u64* __restrict__ bdat, u32 batch, u32 nwg) {
+    OFHE_VGPR_FLOOR();
     static_assert(NR == 2 || NR == 3, "k_block covers the last 8 (NR=2) or 12 (NR=3) stages");
     __shared__ u64 lds[LDS_WORDS];
     const u32 tid = threadIdx.x;
@@ -731,6 +732,7 @@ static_assert(TCOLS_W == 16 || TCOLS_W == 32, "column tile width");
 template <bool INV, bool SPQ, bool SWS = false>
 __global__ __launch_bounds__(16 * TCOLS_W, OFHE_KB_WAVES) void k_tcols(PlanArgs P, const u64* src, u64* dst,
                                                                        u32 batch, u32 nwg, SwSrc SWA) {
+    OFHE_VGPR_FLOOR();
     constexpr u32 N = 1u << 16, S = 256, W = TCOLS_W;
     // Exchange patterns p = tid + 16W k (round 1) and p = 16W h + W k + r
     // (round 2).  The inverse writes the second and reads the first: unpadded,
@@ -837,6 +839,7 @@ __global__ __launch_bounds__(16 * TCOLS_W, OFHE_KB_WAVES) void k_tcols(PlanArgs 
 // ---------------------------------------------------------------------------
 template <bool INV, bool SPQ>
 __global__ __launch_bounds__(512) void k_tcols9(PlanArgs P, const u64* src, u64* dst, u32 batch, u32 nwg) {
+    OFHE_VGPR_FLOOR();
     constexpr u32 N = 1u << 17, S = 256, W = 16, HALF = 16 * 16 * W;  // words per half tile
     __shared__ u64 lds[2 * HALF];
     const u32 tid = threadIdx.x;
@@ -978,6 +981,7 @@ __device__ __forceinline__ void cols_inv_b(u64 (&v)[CPT][E], bool (&b8)[E], cons
 
 template <int KA, bool INV, int CPT, bool SPQ, bool SWS = false>
 __global__ __launch_bounds__(256) void k_cols(PlanArgs P, const u64* src, u64* dst, u32 batch, u32 nwg, SwSrc S) {
+    OFHE_VGPR_FLOOR();
     constexpr int E = 1 << KA;
     constexpr u32 N = 1u << (KA + 12);
     constexpr u32 CB = 16 / CPT;  // column blocks per polynomial
@@ -1062,6 +1066,7 @@ __global__ __launch_bounds__(256) void k_cols(PlanArgs P, const u64* src, u64* d
 template <int MODE, bool SPQ>
 __global__ __launch_bounds__(256) void k_small(PlanArgs P, const u64* src, u64* dst, const u64* __restrict__ bdat,
                                                u32 batch) {
+    OFHE_VGPR_FLOOR();
     __shared__ u64 lds[2048];
     const u32 logn = P.log_n, N = 1u << logn, half = N >> 1;
     const u32 pb = blockIdx.x;

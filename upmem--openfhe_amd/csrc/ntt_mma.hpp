@@ -99,6 +99,7 @@ __device__ __forceinline__ void nm_gemm(const u64 (&xv)[8], const i32x4* fr, u32
 
 __global__ __launch_bounds__(NM_THREADS, 2) void k_block_mma(PlanArgs P, NmArgs Q, const u64* src, u64* dst,
                                                               const u64* __restrict__ bdat, u32 batch, u32 nwg) {
+    OFHE_VGPR_FLOOR();
     constexpr u32 N = 1u << 16;
     __shared__ i32x4 fr[2 * NM_FRAG];          // F_i, V_i (32 KiB)
     __shared__ u64 xb[NM_POLYS * 256];         // exchange buffer (32 KiB)

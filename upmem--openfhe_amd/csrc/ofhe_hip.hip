@@ -18,6 +18,7 @@
 
 #include "internal.hpp"
 #include "ntt_mma.hpp"
+#include "ntt_m16.hpp"
 
 using namespace ofhe;
 
@@ -329,6 +330,8 @@ int ofhe_hip_plan_create(ofhe_ctx_t ctx, uint32_t log_n, uint32_t towers, const 
         // k_block at its 2 waves per SIMD (rejected variants)
         const char* nm = getenv("OFHE_NTT_MMA");
         if (!nm || atoi(nm) == 0) p->nm_state = -1;
+        const char* m16 = getenv("OFHE_BLOCK_M16");  // k_block_m16 (A/B against k_block)
+        if (!m16 || atoi(m16) == 0) p->m16_state = -1;
     }
     hipError_t e = hipSetDevice(ctx->device);
     if (e == hipSuccess) e = hipMalloc(&p->d_tc, sizeof(TowerConst) * towers);
@@ -406,6 +409,7 @@ int ofhe_hip_plan_destroy(ofhe_plan_t p) {
     (void)hipFree(p->d_twist);
     (void)hipFree(p->d_twist_r);
     (void)hipFree(p->d_nm);
+    (void)hipFree(p->d_m16);
     for (auto& kv : p->tabs) (void)hipFree(kv.second);
     delete p;
     return OFHE_OK;
@@ -711,6 +715,48 @@ int ofhe_hip_ntt_inv_range(ofhe_plan_t p, uint32_t t0, uint32_t count, const uin
 // a special-prime N = 2^16 plan (8 MiB per tower); never for other plans or a
 // modulus outside bm_reduce<SPQ>'s range.
 // ---------------------------------------------------------------------------
+// A-operand fragments of v_mfma_i32_32x32x32_i8 for a 16 x 16 map A[out][in]
+// mod q in k_bconv_mma's layout (bconv_mma.hpp): fragment (mt, s), lane l =
+// rr + 32 kh holds row rr of M-tile mt -- output k = 4 mt + 2 dh + (reg >> 3),
+// constant digit reg & 7, with dh = (rr >> 2) & 1, reg = (rr & 3) + 4 (rr >> 3)
+// -- over the K labels (input 4 s + 2 kh + (e >> 3), data digit e & 7): byte e
+// = signed digit of 2^(8 a) A[k][j] mod q.  16 KiB.
+static void frag16(const u64 (*A)[16], u64 q, unsigned char* dst) {
+    u64 pw[8];
+    for (u32 a = 0; a < 8; a++) pw[a] = (u64)(((u128)1 << (8 * a)) % q);
+    for (u32 mt = 0; mt < 4; mt++)
+        for (u32 s = 0; s < 4; s++)
+            for (u32 l = 0; l < 64; l++) {
+                const u32 rr = l & 31, kh = l >> 5;
+                const u32 dh = (rr >> 2) & 1, reg = (rr & 3) + 4 * (rr >> 3);
+                const u32 k = 4 * mt + 2 * dh + (reg >> 3), bd = reg & 7;
+                for (u32 e = 0; e < 16; e++) {
+                    const u32 j = 4 * s + 2 * kh + (e >> 3), a = e & 7;
+                    const u64 z = mulmod(pw[a], A[k][j], q) + DIGIT_BIAS;
+                    dst[(((size_t)mt * 4 + s) * 64 + l) * 16 + e] = (unsigned char)(((z >> (8 * bd)) & 0xFF) ^ 0x80);
+                }
+            }
+}
+
+// bm_reduce<.., SPQ> constants of q, and whether q is in its range
+static bool bm_red_spq(u64 q, BmRed& R) {
+    const unsigned L = msb64(q);
+    const u64 d = (1ull << L) - q;
+    if (!(L >= 33 && d < (1ull << 32) && (((u128)1 << (81 - L)) + 1) * d + ((u128)1 << 49) + 2 * (u128)d < ((u128)1 << L)))
+        return false;
+    R = BmRed{};
+    R.p = q;
+    R.np = 0 - q;
+    const u128 k = (((u128)1 << 80) + q - 1) / q;
+    const u128 bias = k * q;
+    R.bhi = (u64)(bias >> 32) - (1ull << 16);
+    R.blo = (u64)(bias & 0xFFFFFFFFull) + (1ull << 48);
+    R.p2 = 2 * q;
+    R.r60 = (1ull << L) - q;
+    R.r60p = (u64)(L - 32) | ((u64)((1u << (L - 32)) - 1) << 32);
+    return true;
+}
+
 #ifndef OFHE_NM_CHUNK
 #define OFHE_NM_CHUNK 128  // polynomials per workgroup (the batch loop of one group)
 #endif
@@ -721,11 +767,8 @@ static bool nm_ready(ofhe_plan_t p) {
     if (p->log_n != 16 || !p->spq || !p->split8) return false;
     const u32 T = p->towers, N = 1u << 16;
     for (u32 t = 0; t < T; t++) {
-        const u64 q = p->q[t];
-        const unsigned L = msb64(q);
-        const u64 d = (1ull << L) - q;
-        if (!(L >= 33 && d < (1ull << 32) && (((u128)1 << (81 - L)) + 1) * d + ((u128)1 << 49) + 2 * (u128)d < ((u128)1 << L)))
-            return false;
+        BmRed R;
+        if (!bm_red_spq(p->q[t], R)) return false;
     }
     const size_t per_group = 2 * (size_t)NM_FRAG * 16;  // bytes
     const size_t fbytes = (size_t)T * 256 * per_group;
@@ -736,8 +779,6 @@ static bool nm_ready(ofhe_plan_t p) {
         const u64* Tb = &p->tab[(size_t)t * N];
         const u64* TI = &p->itab[(size_t)t * N];
         const u64 scale = mulmod(p->ninv[t], (u64)(((u128)1 << 64) % q), q);
-        u64 pw[8];
-        for (u32 a = 0; a < 8; a++) pw[a] = (u64)(((u128)1 << (8 * a)) % q);
         for (u32 i = 0; i < 256; i++) {
             u64 F[16][16], V[16][16];  // [k][j]
             for (u32 j0 = 0; j0 < 16; j0++) {
@@ -771,35 +812,10 @@ static bool nm_ready(ofhe_plan_t p) {
                     V[k][j0] = mulmod(x[k], scale, q);
                 }
             }
-            for (u32 mat = 0; mat < 2; mat++) {
-                unsigned char* dst = tab.data() + ((size_t)t * 256 + i) * per_group + (size_t)mat * NM_FRAG * 16;
-                const u64(*A)[16] = mat ? V : F;
-                for (u32 mt = 0; mt < 4; mt++)
-                    for (u32 s = 0; s < 4; s++)
-                        for (u32 l = 0; l < 64; l++) {
-                            const u32 rr = l & 31, kh = l >> 5;
-                            const u32 dh = (rr >> 2) & 1, reg = (rr & 3) + 4 * (rr >> 3);
-                            const u32 k = 4 * mt + 2 * dh + (reg >> 3), bd = reg & 7;
-                            for (u32 e = 0; e < 16; e++) {
-                                const u32 j = 4 * s + 2 * kh + (e >> 3), a = e & 7;
-                                const u64 z = mulmod(pw[a], A[k][j], q) + DIGIT_BIAS;
-                                dst[(((size_t)mt * 4 + s) * 64 + l) * 16 + e] = (unsigned char)(((z >> (8 * bd)) & 0xFF) ^ 0x80);
-                            }
-                        }
-            }
+            for (u32 mat = 0; mat < 2; mat++)
+                frag16(mat ? V : F, q, tab.data() + ((size_t)t * 256 + i) * per_group + (size_t)mat * NM_FRAG * 16);
         }
-        BmRed& R = red[t];
-        R = BmRed{};
-        const unsigned L = msb64(q);
-        R.p = q;
-        R.np = 0 - q;
-        const u128 k = (((u128)1 << 80) + q - 1) / q;
-        const u128 bias = k * q;
-        R.bhi = (u64)(bias >> 32) - (1ull << 16);
-        R.blo = (u64)(bias & 0xFFFFFFFFull) + (1ull << 48);
-        R.p2 = 2 * q;
-        R.r60 = (1ull << L) - q;
-        R.r60p = (u64)(L - 32) | ((u64)((1u << (L - 32)) - 1) << 32);
+        (void)bm_red_spq(q, red[t]);
     };
     {
         unsigned nth = std::thread::hardware_concurrency();
@@ -824,9 +840,100 @@ static bool nm_ready(ofhe_plan_t p) {
     return true;
 }
 
-// the fused block pass: k_block_mma when the plan has its table, else k_block
+// k_block_m16 (ntt_m16.hpp) tables of an N = 2^16 special-prime plan, per
+// tower: F[r][j] = w16^(j rev4(r)) and F'[j][r] = w16^(-j rev4(r)) as
+// fragments (w16 = psi^(2N/16)), bm_reduce constants, the forward twist
+// theta_G^j = psi^((2 rev8(G) + 1) j) at element 256 G + j, and the twiddles
+// w256^(+-j0 rev4(r')) at [r'][j0] (w256 = psi^(2N/256)).  Opt-in with
+// OFHE_BLOCK_M16=1 at plan creation (A/B against k_block).
+static bool m16_ready(ofhe_plan_t p) {
+    std::lock_guard<std::mutex> lk(p->m16_mu);
+    if (p->m16_state) return p->m16_state > 0;
+    p->m16_state = -1;
+    if (p->log_n != 16 || !p->spq || !p->split8) return false;
+    const u32 T = p->towers, N = 1u << 16;
+    for (u32 t = 0; t < T; t++) {
+        BmRed R;
+        if (!bm_red_spq(p->q[t], R)) return false;
+    }
+    const size_t fbytes = (size_t)T * 2 * 1024 * 16, rbytes = (size_t)T * sizeof(BmRed);
+    const size_t twords = (size_t)T * N * 2, wwords = (size_t)T * 1024;
+    std::vector<unsigned char> tab(fbytes + rbytes + (twords + wwords) * 8);
+    BmRed* red = reinterpret_cast<BmRed*>(tab.data() + fbytes);
+    u64* twf = reinterpret_cast<u64*>(tab.data() + fbytes + rbytes);
+    u64* w16 = twf + twords;
+    auto build = [&](u32 t) {
+        const u64 q = p->q[t], psi = p->psi[t];
+        const u64 w256 = powmod(psi, 2 * N / 256, q), w16r = powmod(w256, 16, q), w256i = invmod(w256, q);
+        u64 F[16][16], Fi[16][16];
+        for (u32 r = 0; r < 16; r++)
+            for (u32 j = 0; j < 16; j++) {
+                F[r][j] = powmod(w16r, (u64)j * bitrev(r, 4), q);
+                Fi[j][r] = powmod(w16r, (16 - ((u64)j * bitrev(r, 4)) % 16) % 16, q);
+            }
+        frag16(F, q, tab.data() + (size_t)t * 2 * 1024 * 16);
+        frag16(Fi, q, tab.data() + (size_t)t * 2 * 1024 * 16 + 1024 * 16);
+        (void)bm_red_spq(q, red[t]);
+        u64* tf = twf + (size_t)t * N * 2;
+        for (u32 G = 0; G < 256; G++) {
+            const u64 th = powmod(psi, 2 * (u64)bitrev(G, 8) + 1, q);
+            u64 f = 1;
+            for (u32 j = 0; j < 256; j++) {
+                tf[2 * (G * 256 + j)] = f;
+                tf[2 * (G * 256 + j) + 1] = shoup_pre(f, q);
+                f = mulmod(f, th, q);
+            }
+        }
+        u64* wf = w16 + (size_t)t * 1024;
+        for (u32 r1 = 0; r1 < 16; r1++)
+            for (u32 j0 = 0; j0 < 16; j0++) {
+                const u64 e = (u64)j0 * bitrev(r1, 4);
+                const u64 x = powmod(w256, e, q), y = powmod(w256i, e, q);
+                wf[2 * (r1 * 16 + j0)] = x;
+                wf[2 * (r1 * 16 + j0) + 1] = shoup_pre(x, q);
+                wf[512 + 2 * (r1 * 16 + j0)] = y;
+                wf[512 + 2 * (r1 * 16 + j0) + 1] = shoup_pre(y, q);
+            }
+    };
+    {
+        unsigned nth = std::thread::hardware_concurrency();
+        if (nth < 1) nth = 1;
+        if (nth > T) nth = T;
+        if (nth > 16) nth = 16;
+        std::vector<std::thread> th;
+        for (unsigned w = 0; w < nth; w++)
+            th.emplace_back([&, w] {
+                for (u32 t = w; t < T; t += nth) build(t);
+            });
+        for (auto& x : th) x.join();
+    }
+    void* d = nullptr;
+    if (hipMalloc(&d, tab.size()) != hipSuccess) return false;
+    if (upload_blocking(d, tab.data(), tab.size()) != hipSuccess) {
+        (void)hipFree(d);
+        return false;
+    }
+    p->d_m16 = d;
+    p->m16_state = 1;
+    return true;
+}
+
+// the fused block pass: k_block_m16 or k_block_mma when the plan has their
+// tables (opt-in), else k_block
 static void launch_fused_block(ofhe_plan_t p, const PlanArgs& a, const u64* src, u64* dst, const u64* b, u32 batch,
                                hipStream_t s) {
+    if (m16_ready(p)) {
+        const u32 T = p->towers, N = 1u << 16;
+        const unsigned char* base = reinterpret_cast<const unsigned char*>(p->d_m16);
+        M16Args Q;
+        Q.frag = reinterpret_cast<const i32x4*>(base);
+        Q.red = reinterpret_cast<const BmRed*>(base + (size_t)T * 2 * 1024 * 16);
+        Q.twf = reinterpret_cast<const u64*>(base + (size_t)T * 2 * 1024 * 16 + (size_t)T * sizeof(BmRed));
+        Q.w16 = Q.twf + (size_t)T * N * 2;
+        const u32 nwg = batch * T * 8;
+        hipLaunchKernelGGL(k_block_m16, dim3(nwg), dim3(M16_THREADS), 0, s, a, Q, src, dst, b, batch, nwg);
+        return;
+    }
     if (!nm_ready(p)) {
         launch_block<MODE_FUSED>(a, p->spq, src, dst, b, batch, s, p->split8);
         return;
