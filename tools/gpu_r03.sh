@@ -21,7 +21,7 @@ for step in ${STEPS}; do
                     "tests/test_gpu_parity.py::test_block_m16_vs_oracle" ;;
         newtests) run newtests 500 python -u -m pytest -q --timeout 300 --timeout-method thread \
                     tests/test_gpu_headline_shapes.py "tests/test_gpu_rescale.py::test_rescale_rejects_unsafe_aliasing" ;;
-        ab) run ab 300 env EXP_CONFIGS=";OFHE_BLOCK_M16=1" EXP_BATCH=${AB_BATCH:-256} EXP_ROUNDS=${AB_ROUNDS:-6} \
+        ab) run ab 300 env EXP_CONFIGS="${AB_CONFIGS-;OFHE_BLOCK_M16=1}" EXP_BATCH=${AB_BATCH:-256} EXP_ROUNDS=${AB_ROUNDS:-6} \
                     python -u tools/exp_variants.py ;;
         suite) run suite 900 python -u -m pytest tests -m gpu -q -rf --timeout 300 --timeout-method thread ;;
         bench) run bench 400 python bench.py ${BENCH_ARGS} ;;
