@@ -330,11 +330,13 @@ def test_special_prime_switch_identical(hip, O, monkeypatch):
     assert np.array_equal(outs[0], O.ntt_mul_intt(a, b, O.Tables(n, qs, rs)))
 
 
+@pytest.mark.parametrize("split", ["OFHE_SPLIT9", "OFHE_SPLIT89"])
 @pytest.mark.parametrize("edge", [False, True])
-def test_split9_n17_vs_oracle(hip, O, monkeypatch, edge):
+def test_split9_n17_vs_oracle(hip, O, monkeypatch, edge, split):
     """N = 2^17 under OFHE_SPLIT9 (k_tcols9: 9 column stages + the 8-stage
-    block pass) gives the oracle's forward, inverse and pipeline outputs; edge
-    = all-(q-1) inputs (lazy-reduction corners of the extra stage)."""
+    block pass) and OFHE_SPLIT89 (k_tcols' 8 column stages on 512 columns +
+    the 9-stage block pass) gives the oracle's forward, inverse and pipeline
+    outputs; edge = all-(q-1) inputs (lazy-reduction corners of the split)."""
     import torch
 
     H, ctx = hip
@@ -347,7 +349,7 @@ def test_split9_n17_vs_oracle(hip, O, monkeypatch, edge):
     else:
         a = O.uniform_dcrt(B, T, n, qs, 17)
     b = O.uniform_dcrt(B, T, n, qs, 18)
-    monkeypatch.setenv("OFHE_SPLIT9", "1")
+    monkeypatch.setenv(split, "1")
     plan = H.NTTPlan(ctx, log_n, qs, rs)
     xa, xb = dev(a), dev(b)
     xc = torch.empty_like(xa)

@@ -52,15 +52,17 @@ for p in paths:
     assert L.ofhe_hip_init(0, ctypes.byref(ctx)) == 0
     # EXP_TOGGLE=VAR: a second engine per library built with VAR=1 (plan-creation
     # switches such as OFHE_SPLIT4), timed in the same interleaved rounds
+    # (EXP_TOGGLE="VAR=v;VAR2" adds one engine per entry; a bare VAR means VAR=1)
     toggle = os.environ.get("EXP_TOGGLE")
-    for tv in ([None, toggle] if toggle else [None]):
+    for tv in [None] + (toggle.split(";") if toggle else []):
         if tv:
-            os.environ[tv] = "1"
+            tk, _, tval = tv.partition("=")
+            os.environ[tk] = tval or "1"
         ks = vp()
         assert L.ofhe_hip_ks_create(ctx, log_n, sq, arr(allq[:sq]), arr(allr[:sq]), sp, arr(allq[sq:]),
                                     arr(allr[sq:]), dnum, ctypes.byref(ks)) == 0, L.ofhe_hip_last_error()
         if tv:
-            del os.environ[tv]
+            del os.environ[tk]
         libs.append((os.path.basename(p) + (f"+{tv}" if tv else ""), L, ks))
 s = torch.cuda.current_stream()
 spt = vp(s.cuda_stream)

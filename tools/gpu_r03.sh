@@ -23,6 +23,8 @@ for step in ${STEPS}; do
                     tests/test_gpu_headline_shapes.py "tests/test_gpu_rescale.py::test_rescale_rejects_unsafe_aliasing" ;;
         ab) run ab 300 env EXP_CONFIGS="${AB_CONFIGS-;OFHE_BLOCK_M16=1}" EXP_BATCH=${AB_BATCH:-256} EXP_ROUNDS=${AB_ROUNDS:-6} \
                     python -u tools/exp_variants.py ;;
+        ks) run ks 400 env EXP_TOGGLE="${KS_TOGGLE}" EXP_ROUNDS=${KS_ROUNDS:-8} EXP_ONLY=${KS_ONLY:-libofhe_hip_floor} \
+                    python -u tools/exp_ks.py ;;
         suite) run suite 900 python -u -m pytest tests -m gpu -q -rf --timeout 300 --timeout-method thread ;;
         bench) run bench 400 python bench.py ${BENCH_ARGS} ;;
         pmcm16) run pmcm16 300 env OFHE_BLOCK_M16=1 ./tools/pmc_m16.sh && run pmck16 300 env OFHE_BLOCK_M16=0 ./tools/pmc_m16.sh ;;

@@ -83,10 +83,10 @@ int plan_ntt_range(ofhe_plan_t p, bool inverse, u32 t0, u32 count, const u64* sr
 int plan_ntt_fwd_sub(ofhe_plan_t p, u32 t0, u32 count, u64* y, u64 ystride, const u64* x, u64 xstride, u64* out,
                      u64 ostride, const u64* scal, u32 batch, hipStream_t s, int parts = 3);
 
-// Forward column pass (k_cols plans: 2^12 < N, not split8) of the towers
+// Forward column pass (2^12 < N; not SPLIT_T9) of the towers
 // lifted from `last` ([batch] rows of N, stride lstride, modulus ql; first
 // multiplied by pre mod ql unless pre = 1) and
-// scaled by tab[6 t + 1] (k_cols<.., SWS>), written to y; the block pass
+// scaled by tab[6 t + 1] (k_cols / k_tcols <.., SWS>), written to y; the block pass
 // (plan_ntt_fwd_sub parts = 2) follows.
 int plan_cols_switch(ofhe_plan_t p, u32 t0, u32 count, const u64* last, u64 lstride, u64 ql, u64 pre, const u64* tab,
                      u64* y, u64 ystride, u32 batch, hipStream_t s);
@@ -115,6 +115,14 @@ struct ofhe_ctx_s {
     std::atomic<int> live{1};
 };
 
+enum { SPLIT_COLS = 0, SPLIT_T8 = 1, SPLIT_T9 = 2, SPLIT_T8B9 = 3 };
+// stages of the block pass (its inverse groups have 2^block_stages elements)
+inline uint32_t block_stages(int split, uint32_t log_n) {
+    if (split == SPLIT_T8 || split == SPLIT_T9) return 8;
+    if (split == SPLIT_T8B9) return 9;
+    return log_n < 12 ? log_n : 12;
+}
+
 struct ofhe_plan_s {
     ofhe_ctx_t ctx = nullptr;
     ofhe::u32 log_n = 0, towers = 0;
@@ -132,7 +140,13 @@ struct ofhe_plan_s {
     // and internal streams the chunks alternate over (1 = caller's stream).
     ofhe::u32 chunk_batch = 0, nstreams = 1;
     bool spq = false;     // every modulus is 2^L - d with d < 2^32 (special-prime kernels)
-    bool split8 = false;  // log_n == 16: 8 column stages + 8 block stages (k_tcols + k_block<.,.,2>)
+    // column | block pass split for log_n > 12 (SPLIT_*, ofhe_hip.hip):
+    //   SPLIT_COLS  k_cols (log_n - 12 stages) + k_block NR = 3
+    //   SPLIT_T8    k_tcols (8) + k_block NR = 2            (N = 2^16)
+    //   SPLIT_T9    k_tcols9 (9) + k_block NR = 2           (N = 2^17)
+    //   SPLIT_T8B9  k_tcols (8) + k_block NR = 3 whose first round keeps only
+    //               its last stage (9 block stages)          (N = 2^17)
+    int split = 0;
     hipStream_t st[2] = {nullptr, nullptr};
     hipEvent_t ev_fork = nullptr, ev_join[2] = {nullptr, nullptr};
     std::mutex fork_mu;  // guards st / ev_* (plan_tune, the two-stream pipeline)

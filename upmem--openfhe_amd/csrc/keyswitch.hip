@@ -283,6 +283,7 @@ struct ofhe_ks_s {
     std::vector<u64> q, p;
     ofhe_plan_t plan = nullptr;  // towers q[0..size_q) then p[0..size_p)
     hipStream_t side[KS_NSIDE] = {};  // fork streams (OFHE_KS_STREAMS=1: none)
+    u32 chunk = 0;                    // ciphertexts per ModUp chunk (OFHE_KS_CHUNK; 0: the whole batch)
     std::mutex mu;
     std::map<u32, KsLevel*> levels;
 };
@@ -330,6 +331,8 @@ int ofhe_hip_ks_create(ofhe_ctx_t ctx, uint32_t log_n, uint32_t size_q, const ui
     k->q = mq;
     k->p = mp;
     k->plan = plan;
+    const char* ck = getenv("OFHE_KS_CHUNK");
+    if (ck) k->chunk = (u32)atoi(ck);
     const char* ns = getenv("OFHE_KS_STREAMS");
     if (!(ns && atoi(ns) == 1)) {
         hipError_t e = hipSetDevice(ctx->device);
@@ -526,33 +529,40 @@ static int ks_precompute_impl(ofhe_ks_t k, KsLevel* L, uint32_t size_ql, const u
     KsFork fk;
     RCCHK(fk.open(k, stream));
     const u64 N = 1ull << k->log_n, l = size_ql, P = k->size_p, poly = (l + P) * N, ds = L->beta * poly;
+    // ModUp in chunks of ciphertexts (OFHE_KS_CHUNK), so that a chunk's
+    // converted towers can still sit in the Infinity Cache when its forward
+    // transform reads them
+    const u32 cb = k->chunk && k->chunk < batch ? k->chunk : batch;
+    for (u32 b0 = 0; b0 < batch; b0 += cb)
     for (u32 j = 0; j < L->beta; j++) {
         const u32 st = L->start[j], n = L->cnt[j];
+        const u32 batch_ = std::min(cb, batch - b0);
         hipStream_t s = fk.f[j % KS_NSIDE];  // digits are independent
-        u64* slot = digits + j * poly;
+        u64* slot = digits + (u64)b0 * ds + j * poly;
+        const uint64_t* c_ = c + (u64)b0 * l * N;
         // partsCt[j] in coefficient form (keyswitch-hybrid.cpp:384-385)
-        RCCHK(plan_ntt_range(k->plan, true, st, n, c + st * N, slot + st * N, l * N, ds, batch, s));
+        RCCHK(plan_ntt_range(k->plan, true, st, n, c_ + st * N, slot + st * N, l * N, ds, batch_, s));
         // ApproxSwitchCRTBasis to the complement, written around the digit slot (388-406)
         BconvArgs B = L->up[j]->args;
         B.in_stride = B.out_stride = ds;
         B.gap_at = st;
         B.gap = n;
         B.lazy_out = 1;  // every complement tower goes through a forward NTT below
-        RCCHK(bconv_run(B, slot + st * N, slot, batch, s));
+        RCCHK(bconv_run(B, slot + st * N, slot, batch_, s));
         // complement towers to evaluation form (394)
-        RCCHK(plan_ntt_range(k->plan, false, 0, st, slot, slot, ds, ds, batch, s));
+        RCCHK(plan_ntt_range(k->plan, false, 0, st, slot, slot, ds, ds, batch_, s));
         if (OFHE_KS_MERGE && l == k->size_q) {
             // full level: the Q towers after the digit and the P towers are
             // adjacent both in the plan and in the slot -- one launch
             RCCHK(plan_ntt_range(k->plan, false, st + n, (u32)(l + P) - st - n, slot + (st + n) * N,
-                                 slot + (st + n) * N, ds, ds, batch, s));
+                                 slot + (st + n) * N, ds, ds, batch_, s));
         } else {
             RCCHK(plan_ntt_range(k->plan, false, st + n, (u32)l - st - n, slot + (st + n) * N, slot + (st + n) * N,
-                                 ds, ds, batch, s));
-            RCCHK(plan_ntt_range(k->plan, false, k->size_q, (u32)P, slot + l * N, slot + l * N, ds, ds, batch, s));
+                                 ds, ds, batch_, s));
+            RCCHK(plan_ntt_range(k->plan, false, k->size_q, (u32)P, slot + l * N, slot + l * N, ds, ds, batch_, s));
         }
         // the digit's own towers stay as given (evaluation form, 402-404)
-        if (own_copy) RCCHK(copy_rows(slot + st * N, ds, c + st * N, l * N, (u64)n * N, batch, s));
+        if (own_copy) RCCHK(copy_rows(slot + st * N, ds, c_ + st * N, l * N, (u64)n * N, batch_, s));
     }
     return fk.join();
 }
@@ -794,7 +804,7 @@ static int rescale_run(ofhe_plan_t p, u32 towers, const u64* x, u64 xs, u64* out
     RCCHK(sy.alloc((size_t)batch * L * N * 8, s, p->ctx));
     RCCHK(plan_ntt_range(p, true, L, 1, x + (u64)L * N, sl.w(), xs, N, batch, s));
     const u64 ys = (u64)L * N;
-    if (log_n > 12 && (!p->split8 || log_n == 16) && OFHE_RESCALE_FUSE) {
+    if (log_n > 12 && p->split != SPLIT_T9 && OFHE_RESCALE_FUSE) {
         // the lift happens in the column pass's loads (k_cols<.., SWS>): the
         // switched towers are never written to HBM before their transform
         RCCHK(plan_cols_switch(p, 0, L, sl.w(), N, ql, A.pre, dsw, sy.w(), ys, batch, s));
@@ -881,7 +891,7 @@ int ofhe_hip_bv_precompute(ofhe_plan_t p, uint32_t towers, const uint64_t* c, ui
     RCCHK(sc.alloc((size_t)batch * TN * 8, s, p->ctx));
     RCCHK(plan_ntt_range(p, true, 0, T, c, sc.w(), TN, TN, batch, s));
     const u64 dstride = (u64)T * TN;  // words per batch entry of digits
-    const bool fused = log_n > 12 && (!p->split8 || log_n == 16) && OFHE_RESCALE_FUSE;
+    const bool fused = log_n > 12 && p->split != SPLIT_T9 && OFHE_RESCALE_FUSE;
     const u32 bpr = (u32)((N / 2 + 255) / 256);
     if ((u64)bpr * batch * T >= (1ull << 31)) return fail(OFHE_ERR_ARG, "batch too large for one launch");
     for (u32 i = 0; i < T; i++) {

@@ -228,7 +228,7 @@ __device__ __forceinline__ u64 canon_fwd(u64 x, const Mod<SPQ>& M) {
 //     they sit at fixed register positions, so they cost two adds;
 //   * gives that round wave-uniform twiddles (11 scalars per tower);
 // The block pass runs the DIT stages inside its groups of G = 2^lb elements
-// (lb = 8 under split8, else min(12, logN)); the GS column pass (unchanged)
+// (lb = block_stages(plan split), internal.hpp); the GS column pass (unchanged)
 // runs the rest.  They meet because the GS intermediate after its first lb
 // stages is, for group b and position j0 (checked numerically),
 //   W_b[j0] = psi^-((2 rev(b) + 1) j0) * Z_b[j0],
@@ -524,11 +524,16 @@ __device__ __forceinline__ void wave_stage_out(const u64 (&v)[16], u64* lds, u32
 #ifndef OFHE_KB_WAVES
 #define OFHE_KB_WAVES 4
 #endif
-template <int MODE, bool SPQ, int NR>
+// SK = 3 (NR = 3 only, SPLIT_T8B9): the column pass ran the first three
+// stages of round 1 (strides 2048, 1024, 512), so the forward round 1 keeps
+// its last stage (stride 256) and the inverse round 1' its first (t = 256);
+// the inverse twist is the one of 512-element groups.
+template <int MODE, bool SPQ, int NR, int SK = 0>
 __global__ __launch_bounds__(256, OFHE_KB_WAVES) void k_block(PlanArgs P, const u64* src, u64* dst,
                                                               const u64* __restrict__ bdat, u32 batch, u32 nwg) {
     OFHE_VGPR_FLOOR();
     static_assert(NR == 2 || NR == 3, "k_block covers the last 8 (NR=2) or 12 (NR=3) stages");
+    static_assert(SK == 0 || (SK == 3 && NR == 3), "k_block: SK = 3 needs NR = 3");
     __shared__ u64 lds[LDS_WORDS];
     const u32 tid = threadIdx.x;
     const u32 logn = P.log_n;
@@ -559,7 +564,10 @@ __global__ __launch_bounds__(256, OFHE_KB_WAVES) void k_block(PlanArgs P, const 
             // round 1: st = 256, p = tid + 256k
 #pragma unroll
             for (int k = 0; k < 16; k++) v[k] = ld_s(blk + tid + 256 * k);
-            fwd_round16(v, tw, (N >> 12) + g, M);
+            if (SK == 3)
+                fwd_stage16<3>(v, tw, (N >> 12) + g, M);  // input < 12q (k_tcols) -> < 12q
+            else
+                fwd_round16(v, tw, (N >> 12) + g, M);
 #pragma unroll
             for (int k = 0; k < 16; k++) lds[L1 + 272 * k] = v[k];
             __syncthreads();
@@ -688,7 +696,10 @@ __global__ __launch_bounds__(256, OFHE_KB_WAVES) void k_block(PlanArgs P, const 
     __syncthreads();
 #pragma unroll
     for (int k = 0; k < 16; k++) v[k] = lds[L1 + 272 * k];
-    dit_round16(v, dtw, 256, tid, M);
+    if (SK == 3)
+        dit_stage16<0, 1>(v, dtw + 2 * ((u64)256 + tid), 256, M);  // t = 256 only: < 16q -> < 12q
+    else
+        dit_round16(v, dtw, 256, tid, M);
 #pragma unroll
     for (int k = 0; k < 16; k++) {
         const Tw f = ldtw(tw_, tid + 256 * k);
@@ -729,11 +740,15 @@ constexpr u32 TCOLS_W = OFHE_TCOLS_W;
 #define OFHE_TCOLS_PADF 1
 #endif
 static_assert(TCOLS_W == 16 || TCOLS_W == 32, "column tile width");
-template <bool INV, bool SPQ, bool SWS = false>
+// LOGN = 17 (the 8 | 9 split, SPLIT_T8B9): element j = row * 512 + col, the
+// same 256-row sub-transforms on 512 columns (the twiddle index of stage m is
+// m + row / (256 / m) whatever the row length).
+template <bool INV, bool SPQ, bool SWS = false, int LOGN = 16>
 __global__ __launch_bounds__(16 * TCOLS_W, OFHE_KB_WAVES) void k_tcols(PlanArgs P, const u64* src, u64* dst,
                                                                        u32 batch, u32 nwg, SwSrc SWA) {
     OFHE_VGPR_FLOOR();
-    constexpr u32 N = 1u << 16, S = 256, W = TCOLS_W;
+    static_assert(LOGN == 16 || LOGN == 17, "k_tcols: N = 2^16 or 2^17");
+    constexpr u32 N = 1u << LOGN, S = N / 256, W = TCOLS_W;
     // Exchange patterns p = tid + 16W k (round 1) and p = 16W h + W k + r
     // (round 2).  The inverse writes the second and reads the first: unpadded,
     // both conflict free (SQ_LDS_BANK_CONFLICT = 0; a p + p/16 padding made its

@@ -223,8 +223,11 @@ int ofhe_hip_plan_create(ofhe_ctx_t ctx, uint32_t log_n, uint32_t towers, const 
     // N = 2^16 (k_tcols; OFHE_SPLIT4 restores k_cols + NR = 3).  At N = 2^17
     // the 9 | 8 split (k_tcols9) is opt-in, OFHE_SPLIT9: measured 4 % slower in
     // key switching than k_cols (5 stages) + NR = 3 (rejected variants)
-    const bool split8 =
-        (log_n == 16 && !getenv("OFHE_SPLIT4")) || (log_n == 17 && getenv("OFHE_SPLIT9") != nullptr);
+    // OFHE_SPLIT89 at N = 2^17: k_tcols' 8 stages + a 9-stage block pass
+    int split = SPLIT_COLS;
+    if (log_n == 16 && !getenv("OFHE_SPLIT4")) split = SPLIT_T8;
+    if (log_n == 17 && getenv("OFHE_SPLIT9")) split = SPLIT_T9;
+    if (log_n == 17 && getenv("OFHE_SPLIT89")) split = SPLIT_T8B9;
     // PreCompute (transformnat-impl.h:708-763), one host thread per tower group
     auto build = [&](u32 t) {
         const u64 qt = q[t], ps = psi[t], psinv = invmod(ps, qt);
@@ -274,7 +277,7 @@ int ofhe_hip_plan_create(ofhe_ctx_t ctx, uint32_t log_n, uint32_t towers, const 
             }
             // block-pass twist: group b of G = 2^lb, position j0 ->
             // N^-1 psi^-((2 rev(b) + 1) j0) (ntt_kernels.hpp)
-            const u32 lb = split8 ? 8 : (log_n < 12 ? log_n : 12), G = 1u << lb;
+            const u32 lb = block_stages(split, log_n), G = 1u << lb;
             const u64 R = (u64)(((u128)1 << 64) % qt);
             for (u32 b = 0; b < N / G; b++) {
                 const u64 step = powmod(psinv, 2 * (u64)bitrev(b, log_n - lb) + 1, qt);
@@ -324,7 +327,7 @@ int ofhe_hip_plan_create(ofhe_ctx_t ctx, uint32_t log_n, uint32_t towers, const 
     p->spq = true;
     for (u32 t = 0; t < towers; t++) p->spq = p->spq && tc[t].spq_sh != 0;
     if (getenv("OFHE_NO_SPQ")) p->spq = false;  // A/B switch for tests and timing
-    p->split8 = split8;
+    p->split = split;
     {
         // opt-in (OFHE_NTT_MMA=1): k_block_mma measured 1.7x slower than
         // k_block at its 2 waves per SIMD (rejected variants)
@@ -508,29 +511,45 @@ static void launch_cols(const PlanArgs& a, bool spq, bool inv, const u64* src, u
         launch_cols_s<false>(a, inv, src, dst, batch, s);
 }
 
-// column pass for log_n > 12: k_tcols / k_tcols9 (8 / 9 stages) under split8, else k_cols
-static void launch_colpass(const PlanArgs& a, bool spq, bool split8, bool inv, const u64* src, u64* dst, u32 batch,
+// column pass for log_n > 12: k_tcols / k_tcols9 (8 / 9 stages) unless SPLIT_COLS, else k_cols
+static void launch_colpass(const PlanArgs& a, bool spq, int split, bool inv, const u64* src, u64* dst, u32 batch,
                            hipStream_t s);
 
-// Pass split for log_n > 12: with split8 (log_n == 16, 17) the column pass does
-// 8 (k_tcols) or 9 (k_tcols9) stages and the block pass the last 8 (k_block
-// NR=2); otherwise the
-// column pass does log_n - 12 stages in registers (k_cols) and the block pass 12.
+// Pass split for log_n > 12 (the plan's split, internal.hpp): the block pass
+// runs the last 8 (SPLIT_T8 / T9: k_block NR = 2), 9 (SPLIT_T8B9: NR = 3
+// without the first three stages of its first round) or 12 stages.
 template <int MODE>
 static void launch_block(const PlanArgs& a, bool spq, const u64* src, u64* dst, const u64* b, u32 batch,
-                         hipStream_t s, bool split8 = false) {
+                         hipStream_t s, int split = SPLIT_COLS) {
     const u32 nwg = batch * a.towers * (1u << (a.log_n - 12));
-#define LB(SP, NR) hipLaunchKernelGGL((k_block<MODE, SP, NR>), dim3(nwg), dim3(256), 0, s, a, src, dst, b, batch, nwg)
-    if (split8) {
-        if (spq) LB(true, 2); else LB(false, 2);
+#define LB(SP, NR, SK) \
+    hipLaunchKernelGGL((k_block<MODE, SP, NR, SK>), dim3(nwg), dim3(256), 0, s, a, src, dst, b, batch, nwg)
+    if (split == SPLIT_T8 || split == SPLIT_T9) {
+        if (spq) LB(true, 2, 0); else LB(false, 2, 0);
+    } else if (split == SPLIT_T8B9) {
+        if (spq) LB(true, 3, 3); else LB(false, 3, 3);
     } else {
-        if (spq) LB(true, 3); else LB(false, 3);
+        if (spq) LB(true, 3, 0); else LB(false, 3, 0);
     }
 #undef LB
 }
 
-static void launch_tcols(const PlanArgs& a, bool spq, bool inv, const u64* src, u64* dst, u32 batch, hipStream_t s) {
-    if (a.log_n == 17) {
+static void launch_tcols(const PlanArgs& a, bool spq, int split, bool inv, const u64* src, u64* dst, u32 batch,
+                         hipStream_t s) {
+    if (split == SPLIT_T8B9) {
+        const u32 nwg = batch * a.towers * (512 / TCOLS_W);
+#define LT17(I, SP)                                                                                           \
+    hipLaunchKernelGGL((k_tcols<I, SP, false, 17>), dim3(nwg), dim3(16 * TCOLS_W), 0, s, a, src, dst, batch, nwg, \
+                       SwSrc{nullptr, 0, 0, nullptr, 1, 0})
+        if (inv) {
+            if (spq) LT17(true, true); else LT17(true, false);
+        } else {
+            if (spq) LT17(false, true); else LT17(false, false);
+        }
+#undef LT17
+        return;
+    }
+    if (split == SPLIT_T9) {
         const u32 nwg = batch * a.towers * 16;  // 16-column tiles of 512 rows
 #define LT9(I, SP) hipLaunchKernelGGL((k_tcols9<I, SP>), dim3(nwg), dim3(512), 0, s, a, src, dst, batch, nwg)
         if (inv) {
@@ -564,10 +583,10 @@ static void launch_small(const PlanArgs& a, bool spq, const u64* src, u64* dst, 
         hipLaunchKernelGGL((k_small<MODE, false>), dim3(batch * a.towers), dim3(thr), 0, s, a, src, dst, b, batch);
 }
 
-static void launch_colpass(const PlanArgs& a, bool spq, bool split8, bool inv, const u64* src, u64* dst, u32 batch,
+static void launch_colpass(const PlanArgs& a, bool spq, int split, bool inv, const u64* src, u64* dst, u32 batch,
                            hipStream_t s) {
-    if (split8)
-        launch_tcols(a, spq, inv, src, dst, batch, s);
+    if (split != SPLIT_COLS)
+        launch_tcols(a, spq, split, inv, src, dst, batch, s);
     else
         launch_cols(a, spq, inv, src, dst, batch, s);
 }
@@ -593,17 +612,17 @@ int plan_ntt_range(ofhe_plan_t p, bool inverse, u32 t0, u32 count, const u64* sr
         if (p->log_n < 12) {
             launch_small<MODE_FWD>(a, p->spq, src, dst, nullptr, batch, s);
         } else if (p->log_n == 12) {
-            launch_block<MODE_FWD>(a, p->spq, src, dst, nullptr, batch, s, p->split8);
+            launch_block<MODE_FWD>(a, p->spq, src, dst, nullptr, batch, s, p->split);
         } else {
-            launch_colpass(a, p->spq, p->split8, false, src, dst, batch, s);
-            launch_block<MODE_FWD>(ad, p->spq, dst, dst, nullptr, batch, s, p->split8);
+            launch_colpass(a, p->spq, p->split, false, src, dst, batch, s);
+            launch_block<MODE_FWD>(ad, p->spq, dst, dst, nullptr, batch, s, p->split);
         }
     } else {
         if (p->log_n < 12) {
             launch_small<MODE_INV>(a, p->spq, src, dst, nullptr, batch, s);
         } else {
-            launch_block<MODE_INV>(a, p->spq, src, dst, nullptr, batch, s, p->split8);
-            if (p->log_n > 12) launch_colpass(ad, p->spq, p->split8, true, dst, dst, batch, s);
+            launch_block<MODE_INV>(a, p->spq, src, dst, nullptr, batch, s, p->split);
+            if (p->log_n > 12) launch_colpass(ad, p->spq, p->split, true, dst, dst, batch, s);
         }
     }
     return post_launch();
@@ -612,20 +631,30 @@ int plan_ntt_range(ofhe_plan_t p, bool inverse, u32 t0, u32 count, const u64* sr
 int plan_cols_switch(ofhe_plan_t p, u32 t0, u32 count, const u64* last, u64 lstride, u64 ql, u64 pre, const u64* tab,
                      u64* y, u64 ystride, u32 batch, hipStream_t s) {
     if (!p || !p->ctx) return fail(OFHE_ERR_STATE, "plan is NULL or destroyed");
-    if (p->log_n <= 12 || (p->split8 && p->log_n != 16)) return fail(OFHE_ERR_ARG, "plan_cols_switch: k_cols / k_tcols plans only");
+    if (p->log_n <= 12 || p->split == SPLIT_T9) return fail(OFHE_ERR_ARG, "plan_cols_switch: k_cols / k_tcols plans only");
     if (((uintptr_t)last & 15) || (lstride & 1)) return fail(OFHE_ERR_ARG, "plan_cols_switch: misaligned source");
     HIPCHK(hipSetDevice(p->ctx->device));
     PlanArgs a = args_of(p, t0, count);
     a.sstride = a.dstride = ystride;
     pre %= ql;
     const SwSrc S{last, lstride, ql, tab, pre, pre == 1 ? 0 : shoup_pre(pre, ql)};
-    if (p->split8) {  // N = 2^16: k_tcols
+    if (p->split == SPLIT_T8) {  // N = 2^16: k_tcols
         const u32 nwg = batch * a.towers * (256 / TCOLS_W);
         if (p->spq)
             hipLaunchKernelGGL((k_tcols<false, true, true>), dim3(nwg), dim3(16 * TCOLS_W), 0, s, a,
                                (const u64*)nullptr, y, batch, nwg, S);
         else
             hipLaunchKernelGGL((k_tcols<false, false, true>), dim3(nwg), dim3(16 * TCOLS_W), 0, s, a,
+                               (const u64*)nullptr, y, batch, nwg, S);
+        return post_launch();
+    }
+    if (p->split == SPLIT_T8B9) {  // N = 2^17: k_tcols, 512 columns
+        const u32 nwg = batch * a.towers * (512 / TCOLS_W);
+        if (p->spq)
+            hipLaunchKernelGGL((k_tcols<false, true, true, 17>), dim3(nwg), dim3(16 * TCOLS_W), 0, s, a,
+                               (const u64*)nullptr, y, batch, nwg, S);
+        else
+            hipLaunchKernelGGL((k_tcols<false, false, true, 17>), dim3(nwg), dim3(16 * TCOLS_W), 0, s, a,
                                (const u64*)nullptr, y, batch, nwg, S);
         return post_launch();
     }
@@ -650,7 +679,7 @@ int plan_ntt_fwd_block(ofhe_plan_t p, u32 t0, u32 count, u64* y, u64 ystride, u3
     HIPCHK(hipSetDevice(p->ctx->device));
     PlanArgs a = args_of(p, t0, count);
     a.sstride = a.dstride = ystride;
-    launch_block<MODE_FWD>(a, p->spq, y, y, nullptr, batch, s, p->split8);
+    launch_block<MODE_FWD>(a, p->spq, y, y, nullptr, batch, s, p->split);
     return post_launch();
 }
 
@@ -663,14 +692,14 @@ int plan_ntt_fwd_sub(ofhe_plan_t p, u32 t0, u32 count, u64* y, u64 ystride, cons
     HIPCHK(hipSetDevice(p->ctx->device));
     PlanArgs a = args_of(p, t0, count);
     a.sstride = a.dstride = ystride;
-    if (p->log_n > 12 && (parts & 1)) launch_colpass(a, p->spq, p->split8, false, y, y, batch, s);
+    if (p->log_n > 12 && (parts & 1)) launch_colpass(a, p->spq, p->split, false, y, y, batch, s);
     if (!(parts & 2)) return post_launch();
     PlanArgs ab = a;
     ab.sstride = ystride;
     ab.dstride = ostride;
     ab.bstride = xstride;
     ab.scal = scal;
-    launch_block<MODE_FWD_SUB>(ab, p->spq, y, out, x, batch, s, p->split8);
+    launch_block<MODE_FWD_SUB>(ab, p->spq, y, out, x, batch, s, p->split);
     return post_launch();
 }
 }  // namespace ofhe
@@ -764,7 +793,7 @@ static bool nm_ready(ofhe_plan_t p) {
     std::lock_guard<std::mutex> lk(p->nm_mu);
     if (p->nm_state) return p->nm_state > 0;
     p->nm_state = -1;
-    if (p->log_n != 16 || !p->spq || !p->split8) return false;
+    if (p->log_n != 16 || !p->spq || !p->split) return false;
     const u32 T = p->towers, N = 1u << 16;
     for (u32 t = 0; t < T; t++) {
         BmRed R;
@@ -850,7 +879,7 @@ static bool m16_ready(ofhe_plan_t p) {
     std::lock_guard<std::mutex> lk(p->m16_mu);
     if (p->m16_state) return p->m16_state > 0;
     p->m16_state = -1;
-    if (p->log_n != 16 || !p->spq || !p->split8) return false;
+    if (p->log_n != 16 || !p->spq || !p->split) return false;
     const u32 T = p->towers, N = 1u << 16;
     for (u32 t = 0; t < T; t++) {
         BmRed R;
@@ -935,7 +964,7 @@ static void launch_fused_block(ofhe_plan_t p, const PlanArgs& a, const u64* src,
         return;
     }
     if (!nm_ready(p)) {
-        launch_block<MODE_FUSED>(a, p->spq, src, dst, b, batch, s, p->split8);
+        launch_block<MODE_FUSED>(a, p->spq, src, dst, b, batch, s, p->split);
         return;
     }
     NmArgs Q;
@@ -961,7 +990,7 @@ int ofhe_hip_ntt_mul_intt(ofhe_plan_t p, const uint64_t* a_, const uint64_t* b, 
     if (p->log_n < 12) {
         launch_small<MODE_FUSED>(a, p->spq, a_, c, b, batch, s);
     } else if (p->log_n == 12) {
-        launch_block<MODE_FUSED>(a, p->spq, a_, c, b, batch, s, p->split8);
+        launch_block<MODE_FUSED>(a, p->spq, a_, c, b, batch, s, p->split);
     } else {
         // Chunk the batch so a chunk's intermediates stay in the Infinity
         // Cache between the three passes; optionally alternate two streams so
@@ -983,9 +1012,9 @@ int ofhe_hip_ntt_mul_intt(ofhe_plan_t p, const uint64_t* a_, const uint64_t* b, 
             const u32 n = batch - b0 < cb ? batch - b0 : cb;
             hipStream_t sx = multi ? p->st[idx & 1] : s;
             const u64 off = (u64)b0 * words;
-            launch_colpass(a, p->spq, p->split8, false, a_ + off, c + off, n, sx);
+            launch_colpass(a, p->spq, p->split, false, a_ + off, c + off, n, sx);
             launch_fused_block(p, a, c + off, c + off, b + off, n, sx);
-            launch_colpass(a, p->spq, p->split8, true, c + off, c + off, n, sx);
+            launch_colpass(a, p->spq, p->split, true, c + off, c + off, n, sx);
         }
         if (multi) {
             for (int i = 0; i < 2; i++) {
@@ -1009,13 +1038,13 @@ int ofhe_hip_ntt_mul_intt_stage(ofhe_plan_t p, int stage, const uint64_t* a_, co
     if (p->log_n < 12) {
         if (stage == 1) launch_small<MODE_FUSED>(a, p->spq, a_, c, b, batch, s);
     } else if (p->log_n == 12) {
-        if (stage == 1) launch_block<MODE_FUSED>(a, p->spq, a_, c, b, batch, s, p->split8);
+        if (stage == 1) launch_block<MODE_FUSED>(a, p->spq, a_, c, b, batch, s, p->split);
     } else if (stage == 0) {
-        launch_colpass(a, p->spq, p->split8, false, a_, c, batch, s);
+        launch_colpass(a, p->spq, p->split, false, a_, c, batch, s);
     } else if (stage == 1) {
         launch_fused_block(p, a, c, c, b, batch, s);
     } else {
-        launch_colpass(a, p->spq, p->split8, true, c, c, batch, s);
+        launch_colpass(a, p->spq, p->split, true, c, c, batch, s);
     }
     return post_launch();
 }
