@@ -603,19 +603,22 @@ __global__ __launch_bounds__(256, OFHE_KB_WAVES) void k_block(PlanArgs P, const 
         } else {
             fwd_round16(v, tw, (N >> 4) + g * 256 + tid, M);
         }
-        if (!(MODE == MODE_FUSED && kMontFused)) {
+        if (!(MODE == MODE_FUSED && kMontFused) && MODE != MODE_FWD_SUB) {
 #pragma unroll
             for (int k = 0; k < 16; k++) v[k] = canon_fwd<SPQ>(v[k], M);
         }
         if (MODE == MODE_FWD_SUB) {
+            // (x - NTT(y)) s mod q without canonicalising NTT(y) first: v < 12q
+            // (round 3 ends with a CS stage), so d = x + 12q - v is in (0, 13q)
+            // < 2^64, the lazy Shoup takes any 64-bit input to [0, 4q), and one
+            // canonicalisation gives the same residue as ModSubFastEq followed
+            // by ModMulFastConstEq (~10 instructions per coefficient fewer)
             u64 xx[16];
             wave_stage_in_pre<BPF>(bdat + boff + (tid >> 6) * 1024, lds, tid, bpre, xx);
             const u64 sc = P.scal[3 * t + 1], scp = P.scal[3 * t + 2];
+            const u64 q12 = M.q8 + M.q4;
 #pragma unroll
-            for (int k = 0; k < 16; k++) {
-                const u64 d = xx[k] < v[k] ? xx[k] + q - v[k] : xx[k] - v[k];  // ModSubFastEq
-                v[k] = shoup_canon(d, sc, scp, q);
-            }
+            for (int k = 0; k < 16; k++) v[k] = canon4m(shoup_lazy(xx[k] + q12 - v[k], sc, scp, M), M);
             wave_stage_out(v, lds, tid, oblk + (tid >> 6) * 1024);
             return;
         }
