@@ -60,7 +60,8 @@ sp = vp(s.cuda_stream)
 times = {nm: {0: [], 1: [], 2: [], "all": [], "fwd": [], "inv": []} for nm, _, _ in libs}
 ref = None
 for rnd in range(int(os.environ.get("EXP_ROUNDS", "6"))):
-    for nm, L, plan in libs:
+    # alternate the order every round (the first engine of a round has an edge)
+    for nm, L, plan in (libs if rnd % 2 == 0 else libs[::-1]):
         for st in (0, 1, 2, "all"):
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             if st == 0 or st == "all":
