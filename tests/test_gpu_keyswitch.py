@@ -361,6 +361,37 @@ def test_keyswitch_bootstrap_shape(hip):
     assert np.array_equal(host(o0), r0) and np.array_equal(host(o1), r1)
 
 
+@pytest.mark.parametrize("sq,sp,dnum,generic,B,cases", [
+    (48, 16, 3, False, 2, ((48, 0), (47, 0))),   # configs[4]; level 47: ModDown fused, ModUp not
+    (12, 4, 3, False, 1, ((12, 0), (12, 65537), (11, 0))),
+    (8, 4, 2, True, 2, ((8, 0), (7, 65537))),     # generic moduli: Mod<false>, no special-prime fold
+])
+def test_keyswitch_bconv_cols(hip, monkeypatch, sq, sp, dnum, generic, B, cases):
+    """N = 2^17 KeySwitchCore with OFHE_BCONV_COLS=1: ApproxSwitchCRTBasis fused
+    with the targets' forward column pass (k_bconv_cols) in ModUp (full level)
+    and ModDown (t = 0), bit-exact against the oracle; lower levels and t > 0
+    take the unfused kernels in the same call."""
+    H, ctx = hip
+    import torch
+
+    monkeypatch.setenv("OFHE_BCONV_COLS", "1")
+    n, q, rq, p, rp, kp, ks = _ks_case(H, ctx, 17, sq, sp, dnum, generic)
+    rng = np.random.default_rng(1700 + sq)
+    kb = _uniform(rng, dnum, q + p, n)
+    ka = _uniform(rng, dnum, q + p, n)
+    dkb, dka = dev(kb), dev(ka)
+    for l, t in cases:
+        c = K.set_format(_uniform(rng, B, q[:l], n), q[:l], rq[:l], True)
+        if l == sq and t == 0:
+            c[0, :, : n // 2] = np.array(q[:l], np.uint64)[:, None] - np.uint64(1)  # largest digits
+        dc = dev(c)
+        o0 = torch.empty((B, l, n), dtype=torch.int64, device="cuda")
+        o1 = torch.empty_like(o0)
+        ks.core(l, dc.data_ptr(), dkb.data_ptr(), dka.data_ptr(), o0.data_ptr(), o1.data_ptr(), t, B, stream())
+        r0, r1 = K.ks_core(kp, c, kb, ka, t)
+        assert np.array_equal(host(o0), r0) and np.array_equal(host(o1), r1), f"level {l} t {t}"
+
+
 @pytest.mark.parametrize("t", [0, 65537])
 def test_mod_down_of_p_times_mod_up_full_size(hip, t):
     """Size-independent identity at N = 2^16, 16 towers: ModDown(P * ModUp(x)) = x."""

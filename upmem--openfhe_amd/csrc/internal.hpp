@@ -83,6 +83,14 @@ int plan_ntt_range(ofhe_plan_t p, bool inverse, u32 t0, u32 count, const u64* sr
 int plan_ntt_fwd_sub(ofhe_plan_t p, u32 t0, u32 count, u64* y, u64 ystride, const u64* x, u64 xstride, u64* out,
                      u64 ostride, const u64* scal, u32 batch, hipStream_t s, int parts = 3);
 
+// ApproxSwitchCRTBasis fused with the targets' forward column pass
+// (k_bconv_cols, bconv_cols.hpp): N = 2^17, SPLIT_COLS plans, <= 16 sources.
+// Target j is written (column-pass output, the block pass's input) at tower
+// j (+ B.gap from B.gap_at on) of `out`, transformed with plan tower t0 + that
+// index.  bconv_cols_ok says whether it applies.
+bool bconv_cols_ok(ofhe_plan_t p, const BconvArgs& B);
+int bconv_cols_run(ofhe_plan_t p, u32 t0, const BconvArgs& B, const u64* x, u64* out, u32 batch, hipStream_t s);
+
 // Forward column pass (2^12 < N; not SPLIT_T9) of the towers
 // lifted from `last` ([batch] rows of N, stride lstride, modulus ql; first
 // multiplied by pre mod ql unless pre = 1) and

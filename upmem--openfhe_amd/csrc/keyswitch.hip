@@ -116,6 +116,7 @@ struct ModDownArgs {
     const TowerScalar* pinv;       // [size_q]
     const TowerScalar* tinv_p;     // [size_p] or NULL (t = 0)
     const TowerScalar* t_q;        // [size_q] or NULL
+    bool bcols = false;            // k_bconv_cols for the conversion + column pass when it applies
 };
 
 int mod_down_run(const ModDownArgs& A, const u64* x, u64 xstride, u64* out, u64 ostride, u32 batch, hipStream_t s) {
@@ -168,11 +169,17 @@ int mod_down_run2(const ModDownArgs& A, const u64* x0, u64 xstride, u64* out0, u
     B.gap_at = A.size_q;
     B.gap = 0;
     B.lazy_out = 1;  // a forward NTT (after an optional tower scale) follows
-    RCCHK(bconv_run(B, sp.w(), sq.w(), b2, s));
-    if (A.t_q) RCCHK(scale_towers(A.t_q, sq.w(), sq.w(), qs, qs, b2, A.size_q, log_n, s));
     const u64* x1 = x0 + (u64)batch * xstride;
     u64* sq1 = sq.w() + (u64)batch * qs;
     const u64* pinv = reinterpret_cast<const u64*>(A.pinv);
+    if (A.bcols && !A.t_q && bconv_cols_ok(A.plan_q, B)) {
+        // the conversion writes the Q towers' column-pass output directly
+        RCCHK(bconv_cols_run(A.plan_q, A.q0, B, sp.w(), sq.w(), b2, s));
+        RCCHK(plan_ntt_fwd_sub(A.plan_q, A.q0, A.size_q, sq.w(), qs, x0, xstride, out0, ostride, pinv, batch, s, 2));
+        return plan_ntt_fwd_sub(A.plan_q, A.q0, A.size_q, sq1, qs, x1, xstride, out1, ostride, pinv, batch, s, 2);
+    }
+    RCCHK(bconv_run(B, sp.w(), sq.w(), b2, s));
+    if (A.t_q) RCCHK(scale_towers(A.t_q, sq.w(), sq.w(), qs, qs, b2, A.size_q, log_n, s));
     if (log_n >= 12) {
         RCCHK(plan_ntt_fwd_sub(A.plan_q, A.q0, A.size_q, sq.w(), qs, x0, xstride, out0, ostride, pinv, b2, s, 1));
         RCCHK(plan_ntt_fwd_sub(A.plan_q, A.q0, A.size_q, sq.w(), qs, x0, xstride, out0, ostride, pinv, batch, s, 2));
@@ -284,6 +291,7 @@ struct ofhe_ks_s {
     ofhe_plan_t plan = nullptr;  // towers q[0..size_q) then p[0..size_p)
     hipStream_t side[KS_NSIDE] = {};  // fork streams (OFHE_KS_STREAMS=1: none)
     u32 chunk = 0;                    // ciphertexts per ModUp chunk (OFHE_KS_CHUNK; 0: the whole batch)
+    bool bcols = false;               // k_bconv_cols in ModUp / ModDown (OFHE_BCONV_COLS)
     std::mutex mu;
     std::map<u32, KsLevel*> levels;
 };
@@ -331,6 +339,8 @@ int ofhe_hip_ks_create(ofhe_ctx_t ctx, uint32_t log_n, uint32_t size_q, const ui
     k->q = mq;
     k->p = mp;
     k->plan = plan;
+    const char* bcc = getenv("OFHE_BCONV_COLS");
+    k->bcols = bcc && atoi(bcc) != 0;
     const char* ck = getenv("OFHE_KS_CHUNK");
     if (ck) k->chunk = (u32)atoi(ck);
     const char* ns = getenv("OFHE_KS_STREAMS");
@@ -548,6 +558,15 @@ static int ks_precompute_impl(ofhe_ks_t k, KsLevel* L, uint32_t size_ql, const u
         B.gap_at = st;
         B.gap = n;
         B.lazy_out = 1;  // every complement tower goes through a forward NTT below
+        if (k->bcols && l == k->size_q && bconv_cols_ok(k->plan, B)) {
+            // full level (slot towers = plan towers): the conversion writes the
+            // complement's column-pass output, the block passes finish it (394)
+            RCCHK(bconv_cols_run(k->plan, 0, B, slot + st * N, slot, batch_, s));
+            if (st) RCCHK(plan_ntt_fwd_block(k->plan, 0, st, slot, ds, batch_, s));
+            RCCHK(plan_ntt_fwd_block(k->plan, st + n, (u32)(l + P) - st - n, slot + (st + n) * N, ds, batch_, s));
+            if (own_copy) RCCHK(copy_rows(slot + st * N, ds, c_ + st * N, l * N, (u64)n * N, batch_, s));
+            continue;
+        }
         RCCHK(bconv_run(B, slot + st * N, slot, batch_, s));
         // complement towers to evaluation form (394)
         RCCHK(plan_ntt_range(k->plan, false, 0, st, slot, slot, ds, ds, batch_, s));
@@ -627,7 +646,7 @@ static int ks_mod_down_impl(ofhe_ks_t k, KsLevel* L, const u64* x, u64* out, u64
     if (t) RCCHK(level_t_tables(k, L, t, &tt));
     const u32 l = L->size_ql, P = k->size_p;
     ModDownArgs A{k->plan, k->plan, 0, k->size_q, l, P, L->down->args, L->d_pinv,
-                  tt ? tt : nullptr, tt ? tt + P : nullptr};
+                  tt ? tt : nullptr, tt ? tt + P : nullptr, k->bcols};
     const u64 N = 1ull << k->log_n;
     return mod_down_run(A, x, (u64)(l + P) * N, out, (u64)l * N, batch, s);
 }
@@ -665,7 +684,7 @@ int ofhe_hip_ks_core(ofhe_ks_t k, uint32_t size_ql, const uint64_t* c, const uin
         if (t) RCCHK(level_t_tables(k, L, t, &tt));
         const u32 l = L->size_ql, P = k->size_p;
         ModDownArgs A{k->plan, k->plan, 0, k->size_q, l, P, L->down->args, L->d_pinv,
-                      tt ? tt : nullptr, tt ? tt + P : nullptr};
+                      tt ? tt : nullptr, tt ? tt + P : nullptr, k->bcols};
         return mod_down_run2(A, c0, poly, out0, out1, (u64)l * N, batch, s);
     }
     KsFork fk;  // after dg, ct: joins before they are freed

@@ -19,6 +19,7 @@
 #include "internal.hpp"
 #include "ntt_mma.hpp"
 #include "ntt_m16.hpp"
+#include "bconv_cols.hpp"
 
 using namespace ofhe;
 
@@ -1348,6 +1349,33 @@ int ofhe_hip_bconv_destroy(ofhe_bconv_t b) {
 }
 
 namespace ofhe {
+bool bconv_cols_ok(ofhe_plan_t p, const BconvArgs& B) {
+    return OFHE_BCONV_MMA && p && p->log_n == 17 && B.log_n == 17 && p->split == SPLIT_COLS && B.mm_tab &&
+           B.mm_ks >= 1 && B.mm_ks <= 4 && (B.mm_spq != 0) == p->spq;
+}
+
+int bconv_cols_run(ofhe_plan_t p, u32 t0, const BconvArgs& B, const u64* x, u64* out, u32 batch, hipStream_t s) {
+    if (!bconv_cols_ok(p, B)) return fail(OFHE_ERR_ARG, "internal: k_bconv_cols does not apply");
+    const u64 nwg = (u64)batch * (4096 / BC_COLS);
+    if (nwg >= (1ull << 31)) return fail(OFHE_ERR_ARG, "batch too large");
+    const PlanArgs a = args_of(p, t0);
+    switch (B.mm_ks) {
+#define BCC(K)                                                                                                   \
+    case K:                                                                                                      \
+        if (p->spq)                                                                                              \
+            hipLaunchKernelGGL((k_bconv_cols<K, true>), dim3((u32)nwg), dim3(BC_THREADS), 0, s, B, a, x, out,   \
+                               batch, (u32)nwg);                                                                 \
+        else                                                                                                     \
+            hipLaunchKernelGGL((k_bconv_cols<K, false>), dim3((u32)nwg), dim3(BC_THREADS), 0, s, B, a, x, out,  \
+                               batch, (u32)nwg);                                                                 \
+        break;
+        BCC(1) BCC(2) BCC(3) BCC(4)
+#undef BCC
+        default: break;
+    }
+    return post_launch();
+}
+
 int bconv_run(const BconvArgs& A, const u64* x, u64* out, u32 batch, hipStream_t s) {
     const u64 total = (u64)batch << A.log_n;
     const u64 blocks = (total + 255) / 256;
