@@ -361,20 +361,21 @@ def test_keyswitch_bootstrap_shape(hip):
     assert np.array_equal(host(o0), r0) and np.array_equal(host(o1), r1)
 
 
-@pytest.mark.parametrize("sq,sp,dnum,generic,B,cases", [
-    (48, 16, 3, False, 2, ((48, 0), (47, 0))),   # configs[4]; level 47: ModDown fused, ModUp not
-    (12, 4, 3, False, 1, ((12, 0), (12, 65537), (11, 0))),
-    (8, 4, 2, True, 2, ((8, 0), (7, 65537))),     # generic moduli: Mod<false>, no special-prime fold
+@pytest.mark.parametrize("sq,sp,dnum,generic,B,cases,fused", [
+    (48, 16, 3, False, 2, ((48, 0), (47, 0)), "1"),   # configs[4]; level 47: ModDown fused, ModUp not
+    (48, 16, 3, False, 1, ((48, 0),), "0"),           # the unfused kernels (OFHE_BCONV_COLS=0)
+    (12, 4, 3, False, 1, ((12, 0), (12, 65537), (11, 0)), "1"),
+    (8, 4, 2, True, 2, ((8, 0), (7, 65537)), "1"),     # generic moduli: Mod<false>, no special-prime fold
 ])
-def test_keyswitch_bconv_cols(hip, monkeypatch, sq, sp, dnum, generic, B, cases):
-    """N = 2^17 KeySwitchCore with OFHE_BCONV_COLS=1: ApproxSwitchCRTBasis fused
-    with the targets' forward column pass (k_bconv_cols) in ModUp (full level)
-    and ModDown (t = 0), bit-exact against the oracle; lower levels and t > 0
-    take the unfused kernels in the same call."""
+def test_keyswitch_bconv_cols(hip, monkeypatch, sq, sp, dnum, generic, B, cases, fused):
+    """N = 2^17 KeySwitchCore with ApproxSwitchCRTBasis fused with the targets'
+    forward column pass (k_bconv_cols, the default) in ModUp (full level) and
+    ModDown (t = 0), and with OFHE_BCONV_COLS=0, bit-exact against the oracle;
+    lower levels and t > 0 take the unfused kernels in the same call."""
     H, ctx = hip
     import torch
 
-    monkeypatch.setenv("OFHE_BCONV_COLS", "1")
+    monkeypatch.setenv("OFHE_BCONV_COLS", fused)
     n, q, rq, p, rp, kp, ks = _ks_case(H, ctx, 17, sq, sp, dnum, generic)
     rng = np.random.default_rng(1700 + sq)
     kb = _uniform(rng, dnum, q + p, n)

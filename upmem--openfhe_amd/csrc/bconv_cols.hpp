@@ -31,9 +31,9 @@ namespace ofhe {
 #define OFHE_BCC_STAGE_BAR 1  // scheduling barrier between the column stages (A/B)
 #endif
 #ifndef OFHE_BCC_WAVES
-#define OFHE_BCC_WAVES 6
+#define OFHE_BCC_WAVES 12  // one target tile per wave at 48 targets (A/B: 12 > 6 > 4 waves per workgroup)
 #endif
-constexpr u32 BC_WAVES = OFHE_BCC_WAVES;  // 12 tiles (48 targets) = 2 per wave
+constexpr u32 BC_WAVES = OFHE_BCC_WAVES;
 constexpr u32 BC_THREADS = 64 * BC_WAVES;
 constexpr u32 BC_COLS = 16, BC_ROWS = 32, BC_POS = BC_COLS * BC_ROWS;
 

@@ -291,7 +291,7 @@ struct ofhe_ks_s {
     ofhe_plan_t plan = nullptr;  // towers q[0..size_q) then p[0..size_p)
     hipStream_t side[KS_NSIDE] = {};  // fork streams (OFHE_KS_STREAMS=1: none)
     u32 chunk = 0;                    // ciphertexts per ModUp chunk (OFHE_KS_CHUNK; 0: the whole batch)
-    bool bcols = false;               // k_bconv_cols in ModUp / ModDown (OFHE_BCONV_COLS)
+    bool bcols = true;                // k_bconv_cols in ModUp / ModDown (OFHE_BCONV_COLS=0: off)
     std::mutex mu;
     std::map<u32, KsLevel*> levels;
 };
@@ -339,8 +339,8 @@ int ofhe_hip_ks_create(ofhe_ctx_t ctx, uint32_t log_n, uint32_t size_q, const ui
     k->q = mq;
     k->p = mp;
     k->plan = plan;
-    const char* bcc = getenv("OFHE_BCONV_COLS");
-    k->bcols = bcc && atoi(bcc) != 0;
+    const char* bcc = getenv("OFHE_BCONV_COLS");  // k_bconv_cols (default on; 0: separate kernels, A/B)
+    k->bcols = !(bcc && atoi(bcc) == 0);
     const char* ck = getenv("OFHE_KS_CHUNK");
     if (ck) k->chunk = (u32)atoi(ck);
     const char* ns = getenv("OFHE_KS_STREAMS");
