@@ -85,7 +85,7 @@ def _converter(H, ctx, log_n, src, dst):
 
 
 @pytest.mark.parametrize("log_n,sq,sp,generic", [(5, 3, 2, False), (12, 4, 2, False), (13, 3, 3, True),
-                                                 (16, 4, 2, False)])
+                                                 (16, 4, 2, False), (17, 16, 6, False), (17, 5, 9, True)])
 @pytest.mark.parametrize("eval_form", [True, False])
 def test_approx_mod_up(hip, log_n, sq, sp, generic, eval_form):
     H, ctx = hip
@@ -106,7 +106,8 @@ def test_approx_mod_up(hip, log_n, sq, sp, generic, eval_form):
     assert np.array_equal(host(out), K.approx_mod_up(x, q, rq, p, rp, eval_form))
 
 
-@pytest.mark.parametrize("log_n,sq,sp,generic", [(5, 3, 2, False), (12, 4, 2, True), (14, 5, 3, False)])
+@pytest.mark.parametrize("log_n,sq,sp,generic", [(5, 3, 2, False), (12, 4, 2, True), (14, 5, 3, False),
+                                                 (17, 6, 16, False), (17, 7, 3, True)])
 @pytest.mark.parametrize("t", [0, 65537])
 def test_approx_mod_down(hip, log_n, sq, sp, generic, t):
     H, ctx = hip

@@ -100,6 +100,15 @@ struct Scratch {
     }
 };
 
+// k_bconv_cols unless OFHE_BCONV_COLS=0 (A/B against the separate kernels)
+bool bcols_default() {
+    static const bool on = [] {
+        const char* e = getenv("OFHE_BCONV_COLS");
+        return !(e && atoi(e) == 0);
+    }();
+    return on;
+}
+
 int copy_rows(u64* dst, u64 dstride, const u64* src, u64 sstride, u64 words, u32 rows, hipStream_t s) {
     if (!words || !rows) return OFHE_OK;
     HIPCHK(hipMemcpy2DAsync(dst, dstride * 8, src, sstride * 8, words * 8, rows, hipMemcpyDeviceToDevice, s));
@@ -136,6 +145,12 @@ int mod_down_run(const ModDownArgs& A, const u64* x, u64 xstride, u64* out, u64 
     B.gap_at = A.size_q;
     B.gap = 0;
     B.lazy_out = 1;  // a forward NTT (after an optional tower scale) follows
+    if (A.bcols && !A.t_q && bconv_cols_ok(A.plan_q, B)) {
+        // the conversion writes the Q towers' column-pass output (k_bconv_cols)
+        RCCHK(bconv_cols_run(A.plan_q, A.q0, B, sp.w(), sq.w(), batch, s));
+        return plan_ntt_fwd_sub(A.plan_q, A.q0, A.size_q, sq.w(), qs, x, xstride, out, ostride,
+                                reinterpret_cast<const u64*>(A.pinv), batch, s, 2);
+    }
     RCCHK(bconv_run(B, sp.w(), sq.w(), batch, s));
     if (A.t_q) RCCHK(scale_towers(A.t_q, sq.w(), sq.w(), qs, qs, batch, A.size_q, log_n, s));
     // SetFormat(EVALUATION), then ans_i = (x_i - switched_i) * PInvModq_i
@@ -208,17 +223,24 @@ int ofhe_hip_approx_mod_up(ofhe_plan_t pq, ofhe_plan_t pp, ofhe_bconv_t bc, int 
     BconvArgs B = bc->args;
     B.out_stride = qp;
     B.lazy_out = 1;  // the P towers go through a forward NTT below
+    const u64* src = x;
+    B.in_stride = Q * N;
     if (eval_form) {
         // coefficient copy of x (SetFormat(COEFFICIENT), 1097-1100) into the Q slots
         RCCHK(plan_ntt_range(pq, true, 0, (u32)Q, x, out, Q * N, qp, batch, s));
+        src = out;
         B.in_stride = qp;
-        RCCHK(bconv_run(B, out, out + Q * N, batch, s));
-    } else {
-        B.in_stride = Q * N;
-        RCCHK(bconv_run(B, x, out + Q * N, batch, s));
     }
-    // P towers to evaluation form (1112-1116)
-    RCCHK(plan_ntt_range(pp, false, 0, (u32)P, out + Q * N, out + Q * N, qp, qp, batch, s));
+    if (bcols_default() && bconv_cols_ok(pp, B)) {
+        // the conversion writes the P towers' column-pass output (k_bconv_cols),
+        // the block pass finishes their forward transform (1112-1116)
+        RCCHK(bconv_cols_run(pp, 0, B, src, out + Q * N, batch, s));
+        RCCHK(plan_ntt_fwd_block(pp, 0, (u32)P, out + Q * N, qp, batch, s));
+    } else {
+        RCCHK(bconv_run(B, src, out + Q * N, batch, s));
+        // P towers to evaluation form (1112-1116)
+        RCCHK(plan_ntt_range(pp, false, 0, (u32)P, out + Q * N, out + Q * N, qp, qp, batch, s));
+    }
     // Q towers: the stored evaluation input, or its NTT (1119-1127)
     if (eval_form) return copy_rows(out, qp, x, Q * N, Q * N, batch, s);
     return plan_ntt_range(pq, false, 0, (u32)Q, x, out, Q * N, qp, batch, s);
@@ -265,7 +287,7 @@ int ofhe_hip_approx_mod_down(ofhe_plan_t pq, ofhe_plan_t pp, ofhe_bconv_t bc, co
         }
     }
     const TowerScalar* d = (const TowerScalar*)dtab;
-    ModDownArgs A{pq, pp, 0, 0, Q, P, bc->args, d, t ? d + Q : nullptr, t ? d + Q + P : nullptr};
+    ModDownArgs A{pq, pp, 0, 0, Q, P, bc->args, d, t ? d + Q : nullptr, t ? d + Q + P : nullptr, bcols_default()};
     const u64 N = 1ull << pq->log_n;
     RCCHK(mod_down_run(A, x, (u64)(Q + P) * N, out, (u64)Q * N, batch, s));
     return OFHE_OK;
@@ -340,7 +362,7 @@ int ofhe_hip_ks_create(ofhe_ctx_t ctx, uint32_t log_n, uint32_t size_q, const ui
     k->p = mp;
     k->plan = plan;
     const char* bcc = getenv("OFHE_BCONV_COLS");  // k_bconv_cols (default on; 0: separate kernels, A/B)
-    k->bcols = !(bcc && atoi(bcc) == 0);
+    k->bcols = !(bcc && atoi(bcc) == 0);          // read per engine, so tests can switch it
     const char* ck = getenv("OFHE_KS_CHUNK");
     if (ck) k->chunk = (u32)atoi(ck);
     const char* ns = getenv("OFHE_KS_STREAMS");
