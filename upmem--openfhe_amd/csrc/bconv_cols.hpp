@@ -30,6 +30,9 @@ namespace ofhe {
 #ifndef OFHE_BCC_STAGE_BAR
 #define OFHE_BCC_STAGE_BAR 1  // scheduling barrier between the column stages (A/B)
 #endif
+#ifndef OFHE_BCC_MINW
+#define OFHE_BCC_MINW 3  // waves per SIMD the register budget is sized for
+#endif
 #ifndef OFHE_BCC_WAVES
 #define OFHE_BCC_WAVES 12  // one target tile per wave at 48 targets (A/B: 12 > 6 > 4 waves per workgroup)
 #endif
@@ -38,7 +41,7 @@ constexpr u32 BC_THREADS = 64 * BC_WAVES;
 constexpr u32 BC_COLS = 16, BC_ROWS = 32, BC_POS = BC_COLS * BC_ROWS;
 
 template <int KS, bool SPQ>
-__global__ __launch_bounds__(BC_THREADS, 3) void k_bconv_cols(BconvArgs A, PlanArgs P, const u64* __restrict__ x,
+__global__ __launch_bounds__(BC_THREADS, OFHE_BCC_MINW) void k_bconv_cols(BconvArgs A, PlanArgs P, const u64* __restrict__ x,
                                                            u64* __restrict__ out, u32 batch, u32 nwg) {
     OFHE_VGPR_FLOOR();
     static_assert(KS >= 1 && KS <= 4, "k_bconv_cols: up to 16 source towers (64 KiB of digits)");
@@ -91,6 +94,38 @@ __global__ __launch_bounds__(BC_THREADS, 3) void k_bconv_cols(BconvArgs A, PlanA
     const BmW W = bm_weights();
     const u32 c = lane & 31, h = lane >> 5, col = c & 15, par = c >> 4;
     u64* ob = out + (u64)b * A.out_stride + c0 + col;
+    // 3. (below) the column pass on the lane's rows 2g + par of column col
+    auto colpass = [&](u64(&vv)[16], u32 j) {
+        if (j >= A.size_p) return;  // the partner lane (c ^ 16) has the same h
+        const u32 jo = j >= A.gap_at ? j + A.gap : j;
+        const Mod<SPQ> M = load_mod<SPQ>(P.tc[jo]);
+        const u64* tw = P.tw + (u64)jo * N * 2;
+        // stages s = 0..3 (row distance 16 >> s, g distance 8 >> s); CS at s = 0, 2
+#pragma unroll
+        for (int s = 0; s < 4; s++) {
+            const int hg = 8 >> s;
+#pragma unroll
+            for (int jb = 0; jb < (1 << s); jb++) {
+                const Tw tw_ = ldtw(tw, (1u << s) + jb);
+#pragma unroll
+                for (int g = jb * 2 * hg; g < jb * 2 * hg + hg; g++) ct_bfly_cs(vv[g], vv[g + hg], tw_, M, (s & 1) == 0);
+            }
+            if (OFHE_BCC_STAGE_BAR) __builtin_amdgcn_sched_barrier(0);  // one stage's twiddles in flight
+        }
+        // stage s = 4: rows (2g, 2g + 1) = lanes (c, c ^ 16); par 0 keeps g < 8, par 1 g >= 8
+        u64* oj = ob + (u64)jo * N;
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+            const u64 snd = par ? vv[k] : vv[8 + k];
+            const u64 rcv = pack((u32)__shfl_xor((int)lo32(snd), 16), (u32)__shfl_xor((int)hi32(snd), 16));
+            u64 xv = par ? rcv : vv[k];
+            u64 yv = par ? vv[8 + k] : rcv;
+            const u32 g = k + 8 * par;
+            ct_bfly_cs(xv, yv, ldtw(tw, 16 + g), M, true);  // -> [0, 12q)
+            st_s(oj + (u64)(2 * g) * COLS, xv);
+            st_s(oj + (u64)(2 * g + 1) * COLS, yv);
+        }
+    };
 #pragma unroll 1
     for (u32 T = w; T < tiles; T += BC_WAVES) {
         i32x4 fa[KS];
@@ -127,38 +162,6 @@ __global__ __launch_bounds__(BC_THREADS, 3) void k_bconv_cols(BconvArgs A, PlanA
             asm volatile("" : "+v"(v0[g]), "+v"(v1[g]));
             __builtin_amdgcn_sched_barrier(0);
         }
-        // 3. the column pass on the lane's rows 2g + par of column col
-        auto colpass = [&](u64(&vv)[16], u32 j) {
-            if (j >= A.size_p) return;  // the partner lane (c ^ 16) has the same h
-            const u32 jo = j >= A.gap_at ? j + A.gap : j;
-            const Mod<SPQ> M = load_mod<SPQ>(P.tc[jo]);
-            const u64* tw = P.tw + (u64)jo * N * 2;
-            // stages s = 0..3 (row distance 16 >> s, g distance 8 >> s); CS at s = 0, 2
-#pragma unroll
-            for (int s = 0; s < 4; s++) {
-                const int hg = 8 >> s;
-#pragma unroll
-                for (int jb = 0; jb < (1 << s); jb++) {
-                    const Tw tw_ = ldtw(tw, (1u << s) + jb);
-#pragma unroll
-                    for (int g = jb * 2 * hg; g < jb * 2 * hg + hg; g++) ct_bfly_cs(vv[g], vv[g + hg], tw_, M, (s & 1) == 0);
-                }
-                if (OFHE_BCC_STAGE_BAR) __builtin_amdgcn_sched_barrier(0);  // one stage's twiddles in flight
-            }
-            // stage s = 4: rows (2g, 2g + 1) = lanes (c, c ^ 16); par 0 keeps g < 8, par 1 g >= 8
-            u64* oj = ob + (u64)jo * N;
-#pragma unroll
-            for (int k = 0; k < 8; k++) {
-                const u64 snd = par ? vv[k] : vv[8 + k];
-                const u64 rcv = pack((u32)__shfl_xor((int)lo32(snd), 16), (u32)__shfl_xor((int)hi32(snd), 16));
-                u64 xv = par ? rcv : vv[k];
-                u64 yv = par ? vv[8 + k] : rcv;
-                const u32 g = k + 8 * par;
-                ct_bfly_cs(xv, yv, ldtw(tw, 16 + g), M, true);  // -> [0, 12q)
-                st_s(oj + (u64)(2 * g) * COLS, xv);
-                st_s(oj + (u64)(2 * g + 1) * COLS, yv);
-            }
-        };
         colpass(v0, 4 * T + 2 * h);
         colpass(v1, 4 * T + 2 * h + 1);
     }
