@@ -1356,6 +1356,9 @@ bool bconv_cols_ok(ofhe_plan_t p, const BconvArgs& B) {
 
 int bconv_cols_run(ofhe_plan_t p, u32 t0, const BconvArgs& B, const u64* x, u64* out, u32 batch, hipStream_t s) {
     if (!bconv_cols_ok(p, B)) return fail(OFHE_ERR_ARG, "internal: k_bconv_cols does not apply");
+    // the last target's plan tower (after the output gap) must exist
+    const u64 last = (u64)B.size_p - 1 + (B.size_p - 1 >= B.gap_at ? B.gap : 0);
+    if (t0 + last >= p->towers) return fail(OFHE_ERR_ARG, "internal: k_bconv_cols targets outside the plan");
     const u64 nwg = (u64)batch * (4096 / BC_COLS);
     if (nwg >= (1ull << 31)) return fail(OFHE_ERR_ARG, "batch too large");
     const PlanArgs a = args_of(p, t0);
