@@ -45,8 +45,10 @@ def test_roofline_uses_only_matching_counters(tmp_path, monkeypatch):
     monkeypatch.setattr(bench, "PMC_FILE", str(tmp_path / "none.json"))
     r = bench.make_roofline(13.5, kms, coeffs, 16, 16, 1024)
     assert r["bound"] is None and r["valu"] is None and r["traffic"] is None
-    assert abs(r["frac"] - 24 * coeffs / 13.5e-3 / 8e12) < 1e-9
+    # top level: the dominant kernel's algorithmic bytes over its launch time
     assert r["dominant_kernel"] == "k_block<fused>"
+    assert abs(r["frac"] - 24 * coeffs / 6.8e-3 / 8e12) < 1e-9
+    assert abs(r["pipeline"]["frac"] - 24 * coeffs / 13.5e-3 / 8e12) < 1e-9
     pm = {"build_id": bench.build_id(), "config": {"log_n": 16, "towers": 16, "batch": 1024},
           "kernels": {k: {"hbm_bytes_per_launch": bench.KERNEL_BYTES[k] * coeffs, "valu_insts_per_coeff": ipc,
                           "clock_ghz": 1.6} for k, ipc in zip(kms, (86, 181, 98))}}
@@ -54,14 +56,16 @@ def test_roofline_uses_only_matching_counters(tmp_path, monkeypatch):
     f.write_text(json.dumps(pm))
     monkeypatch.setattr(bench, "PMC_FILE", str(f))
     r = bench.make_roofline(13.5, kms, coeffs, 16, 16, 1024)
-    assert r["counters"] == "matched" and r["bound"] == "valu"
-    assert r["traffic"] == sum(bench.KERNEL_BYTES[k] * coeffs for k in kms)
+    assert r["counters"] == "matched" and r["bound"] == "valu" and r["pipeline"]["bound"] == "valu"
+    assert r["traffic"] == 24 * coeffs
+    assert r["pipeline"]["traffic"] == sum(bench.KERNEL_BYTES[k] * coeffs for k in kms)
     want = (86 + 181 + 98) * coeffs / 64 / (1024 * 1.6e9 * 0.25) * 1e3
-    assert abs(r["valu"]["valu_bound_ms"] - want) < 1e-9
+    assert abs(r["pipeline"]["valu"]["valu_bound_ms"] - want) < 1e-9
+    assert abs(r["valu"]["valu_bound_ms"] - 181 * coeffs / 64 / (1024 * 1.6e9 * 0.25) * 1e3) < 1e-9
     pm["build_id"] = "stale"
     f.write_text(json.dumps(pm))
     r = bench.make_roofline(13.5, kms, coeffs, 16, 16, 1024)
-    assert r["valu"] is None and "stale" in r["counters"]
+    assert r["valu"] is None and r["pipeline"]["valu"] is None and "stale" in r["counters"]
     pm["build_id"] = bench.build_id()
     pm["config"]["batch"] = 256
     f.write_text(json.dumps(pm))

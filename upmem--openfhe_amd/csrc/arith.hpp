@@ -102,7 +102,24 @@ __device__ __forceinline__ u64 csub_s(u64 x, u64 m) {
 #ifndef OFHE_QH_ADDC
 #define OFHE_QH_ADDC 0  // measured: more instructions (add_co + cndmask), kept for reference
 #endif
+template <bool QA = false>
 __device__ __forceinline__ u64 mulhi_approx(u64 a, u64 b) {
+    if (QA) {
+        // the two middle high words summed by add_co / addc_co straight into
+        // an aligned (sum, carry) pair: the 64-bit accumulator of the final
+        // mad without zero-extending moves or a 64-bit add
+        const u32 h1 = __umulhi(lo32(a), hi32(b));
+        const u32 h2 = __umulhi(hi32(a), lo32(b));
+        u32 s, c;
+        asm("v_add_co_u32 %0, vcc, %2, %3\n\t"
+            "v_addc_co_u32 %1, vcc, 0, 0, vcc"
+            : "=&v"(s), "=v"(c)
+            : "v"(h1), "v"(h2)
+            : "vcc");
+        u64 sc = pack(s, c);
+        asm("" : "+v"(sc));
+        return mad32(hi32(a), hi32(b), sc);
+    }
     if (OFHE_QH_ADDC) {
         // the two middle high words summed with an explicit carry word, so the
         // 64-bit accumulator is built by add/carry instead of zero-extending
@@ -132,7 +149,10 @@ __device__ __forceinline__ u64 mulhi_exact(u64 a, u64 b) {
 // cross product lo32(qh) * hi32(2^64-q) is -(lo32(qh) << (L-32)): a shift
 // instead of a multiply.  Every modulus chain OpenFHE builds with
 // FirstPrime/PreviousPrime near 2^L (nbtheory-impl.h:334-379) has this form.
-template <bool SPQ>
+// QA: the Shoup quotient's two middle words summed by add_co/addc into the
+// final mad's accumulator pair (mulhi_approx<true>); chosen per kernel where a
+// same-process A/B measured it faster (OFHE_QA_* in ntt_kernels.hpp)
+template <bool SPQ, bool QA = false>
 struct Mod {
     u64 q;    // modulus, q < 2^60
     u64 q4;   // 4q
@@ -147,9 +167,9 @@ struct Mod {
 // a < 2^64.  Harvey's bound gives [0, 2q) with the exact quotient; the
 // approximate quotient is at most 2 short.  The remainder is formed as
 // lo64(a*w) + lo64(qh*(2^64-q)), so there is no 64-bit subtraction.
-template <bool SPQ>
-__device__ __forceinline__ u64 shoup_lazy(u64 a, u64 w, u64 wp, const Mod<SPQ>& M) {
-    const u64 qh = mulhi_approx(a, wp);
+template <bool SPQ, bool QA>
+__device__ __forceinline__ u64 shoup_lazy(u64 a, u64 w, u64 wp, const Mod<SPQ, QA>& M) {
+    const u64 qh = mulhi_approx<QA>(a, wp);
     u64 s = mad32(lo32(a), lo32(w), 0);
     s = mad32(lo32(qh), lo32(M.nq), s);
     u32 hi;
@@ -202,7 +222,46 @@ __device__ __forceinline__ u64 barrett_ref(u64 a, u64 b, u64 q, u64 mu, u32 n_sh
 //   (t - m*q) / 2^64 = hi64(t) - hi64(m*q) exactly, in (-q, q): adding q
 //   gives (0, 2q) with no carry/borrow test on the low word.
 // qinv = q^-1 mod 2^64.
+//
+// OFHE_MONT2: the same value with the carries taken by add_co/addc instead
+// of zero-extended 64-bit adds (LLVM emitted 9 register moves per product for
+// the form below):
+//   u = a1 b0 + a0 b1 (< 2^64 under the same bounds), t1 = x1 + u0 with
+//   carry c, hi64(t) = a1 b1 + (u1 + c);
+//   hi64(m q) = m1 q1 + hi32(S1) + L1 + carry(lo32(S1) + L0) with
+//   S1 = m1 q0 + hi32(m0 q0) < 2^64 and L = m0 q1 < 2^60 (q < 2^60).
+#ifndef OFHE_MONT2
+#define OFHE_MONT2 0
+#endif
+__device__ __forceinline__ u64 mont_mul2(u64 a, u64 b, u64 q, u64 qinv) {
+    const u64 x = mad32(lo32(a), lo32(b), 0);
+    const u64 u = mad32(hi32(a), lo32(b), mad32(lo32(a), hi32(b), 0));
+    u32 t1, e;
+    asm("v_add_co_u32 %0, vcc, %2, %3\n\t"
+        "v_addc_co_u32 %1, vcc, %4, 0, vcc"
+        : "=&v"(t1), "=v"(e)
+        : "v"(hi32(x)), "v"(lo32(u)), "v"(hi32(u))
+        : "vcc");
+    const u32 t0 = lo32(x);
+    const u64 m0w = mad32(t0, lo32(qinv), 0);
+    const u32 m0 = lo32(m0w), m1 = hi32(m0w) + t0 * hi32(qinv) + t1 * lo32(qinv);
+    const u64 s1 = mad32(m1, lo32(q), (u64)__umulhi(m0, lo32(q)));
+    const u64 l = mad32(m0, hi32(q), 0);
+    u32 k, k2, junk;
+    asm("v_add_co_u32 %2, vcc, %3, %5\n\t"
+        "v_addc_co_u32 %0, vcc, %4, %6, vcc\n\t"
+        "v_addc_co_u32 %1, vcc, 0, 0, vcc"
+        : "=&v"(k), "=&v"(k2), "=&v"(junk)
+        : "v"(lo32(s1)), "v"(hi32(s1)), "v"(lo32(l)), "v"(hi32(l))
+        : "vcc");
+    u64 kk = pack(k, k2);
+    asm("" : "+v"(kk));
+    const u64 h = mad32(m1, hi32(q), kk);               // hi64(m q)
+    const u64 tq = mad32(hi32(a), hi32(b), q);          // a1 b1 + q
+    return tq - h + (u64)e;
+}
 __device__ __forceinline__ u64 mont_mul(u64 a, u64 b, u64 q, u64 qinv) {
+    if (OFHE_MONT2) return mont_mul2(a, b, q, qinv);
     const u64 x = mad32(lo32(a), lo32(b), 0);
     const u64 y = mad32(hi32(a), lo32(b), x >> 32);  // < 1.5*2^63 + 2^32
     const u64 z = mad32(lo32(a), hi32(b), y);        // + < 2^60: no wrap

@@ -98,7 +98,7 @@ __global__ __launch_bounds__(BC_THREADS, OFHE_BCC_MINW) void k_bconv_cols(BconvA
     auto colpass = [&](u64(&vv)[16], u32 j) {
         if (j >= A.size_p) return;  // the partner lane (c ^ 16) has the same h
         const u32 jo = j >= A.gap_at ? j + A.gap : j;
-        const Mod<SPQ> M = load_mod<SPQ>(P.tc[jo]);
+        const auto M = load_mod<SPQ, (bool)OFHE_QA_BCC>(P.tc[jo]);
         const u64* tw = P.tw + (u64)jo * N * 2;
         // stages s = 0..3 (row distance 16 >> s, g distance 8 >> s); CS at s = 0, 2
 #pragma unroll

@@ -47,9 +47,30 @@ struct TowerConst {
     u32 spq_sh;    // msb(q) - 32 when q = 2^msb - d with d < 2^32, else 0
     u64 qinv;      // q^-1 mod 2^64 (Montgomery Hadamard)
 };
-template <bool SPQ>
-__device__ __forceinline__ Mod<SPQ> load_mod(const TowerConst& tc) {
-    return Mod<SPQ>{tc.q, 4 * tc.q, 8 * tc.q, tc.nq, tc.nq4, 0 - 8 * tc.q, tc.spq_sh};
+// Shoup quotient form per kernel (Mod<SPQ, QA>, arith.hpp): add_co/addc into
+// the accumulator pair (1) or zero-extending moves and a 64-bit add (0).
+// Same-process A/B (tools/exp_variants.py) decides each default.
+#ifndef OFHE_QA_TCF
+#define OFHE_QA_TCF 0  // k_tcols forward
+#endif
+#ifndef OFHE_QA_TCI
+#define OFHE_QA_TCI 0  // k_tcols inverse
+#endif
+#ifndef OFHE_QA_BLK
+#define OFHE_QA_BLK 0  // k_block
+#endif
+#ifndef OFHE_QA_CF
+#define OFHE_QA_CF 0  // k_cols forward
+#endif
+#ifndef OFHE_QA_CI
+#define OFHE_QA_CI 0  // k_cols inverse
+#endif
+#ifndef OFHE_QA_BCC
+#define OFHE_QA_BCC 0  // k_bconv_cols
+#endif
+template <bool SPQ, bool QA = false>
+__device__ __forceinline__ Mod<SPQ, QA> load_mod(const TowerConst& tc) {
+    return Mod<SPQ, QA>{tc.q, 4 * tc.q, 8 * tc.q, tc.nq, tc.nq4, 0 - 8 * tc.q, tc.spq_sh};
 }
 
 // Device view of a plan. Twiddles are interleaved (w, w') pairs so one
@@ -143,13 +164,13 @@ __device__ __forceinline__ Tw ldtw(const u64* base, u32 idx) {
 #ifndef OFHE_THR
 #define OFHE_THR 0
 #endif
-template <bool SPQ>
-__device__ __forceinline__ u64 csub_thr8(u64 x, const Mod<SPQ>& M) {
+template <bool SPQ, bool QA>
+__device__ __forceinline__ u64 csub_thr8(u64 x, const Mod<SPQ, QA>& M) {
     const u32 m = (u32)__builtin_amdgcn_sbfe((int)hi32(x), M.sh + 3, 1);
     return x + pack(m & lo32(M.nq8), m & hi32(M.nq8));
 }
-template <bool SPQ>
-__device__ __forceinline__ void ct_bfly_cs(u64& x, u64& y, Tw w, const Mod<SPQ>& M, bool cs) {
+template <bool SPQ, bool QA>
+__device__ __forceinline__ void ct_bfly_cs(u64& x, u64& y, Tw w, const Mod<SPQ, QA>& M, bool cs) {
     const u64 t = shoup_lazy(y, w.w, w.wp, M);  // [0, 4q)
     u64 a;
     if (OFHE_LAZY_FWD)
@@ -189,24 +210,24 @@ __device__ __forceinline__ u64 canon4(u64 x, u64 q) {  // [0, 4q) -> [0, q)
 #ifndef OFHE_SPQ_CANON
 #define OFHE_SPQ_CANON 1
 #endif
-template <bool SPQ>
-__device__ __forceinline__ u64 canon_spq(u64 x, const Mod<SPQ>& M) {
+template <bool SPQ, bool QA>
+__device__ __forceinline__ u64 canon_spq(u64 x, const Mod<SPQ, QA>& M) {
     const u32 qh = hi32(x) >> M.sh;
     const u64 d = (1ull << (M.sh + 32)) - M.q;  // wave-uniform (scalar unit)
     const u64 xm = pack(lo32(x), hi32(x) & ((1u << M.sh) - 1));
     return csub_s(mad32(qh, lo32(d), xm), M.q);
 }
-template <bool SPQ>
-__device__ __forceinline__ u64 canon8m(u64 x, const Mod<SPQ>& M) {  // [0, 8q) -> [0, q)
+template <bool SPQ, bool QA>
+__device__ __forceinline__ u64 canon8m(u64 x, const Mod<SPQ, QA>& M) {  // [0, 8q) -> [0, q)
     return (SPQ && OFHE_SPQ_CANON) ? canon_spq(x, M) : canon8(x, M.q);
 }
-template <bool SPQ>
-__device__ __forceinline__ u64 canon4m(u64 x, const Mod<SPQ>& M) {  // [0, 4q) -> [0, q)
+template <bool SPQ, bool QA>
+__device__ __forceinline__ u64 canon4m(u64 x, const Mod<SPQ, QA>& M) {  // [0, 4q) -> [0, q)
     return (SPQ && OFHE_SPQ_CANON) ? canon_spq(x, M) : canon4(x, M.q);
 }
 // forward-transform output (any stage pattern) -> [0, q)
-template <bool SPQ>
-__device__ __forceinline__ u64 canon_fwd(u64 x, const Mod<SPQ>& M) {
+template <bool SPQ, bool QA>
+__device__ __forceinline__ u64 canon_fwd(u64 x, const Mod<SPQ, QA>& M) {
     if (SPQ && OFHE_SPQ_CANON && !OFHE_THR) return canon_spq(x, M);  // < 16q < 2^(L+4)
     const u64 q = M.q;
     if (SPQ && OFHE_THR) x = csub_s(x, 8 * q);  // [0, 2^(L+3) + 8q) -> [0, 8q + 8d)
@@ -273,8 +294,8 @@ __device__ __forceinline__ void dit_round16(u64 (&v)[16], const u64* dtw, u32 st
 // dtw[t + j] are the same for every thread, j = 0 is w = 1.
 //   t = 1: all trivial, -> < 4q;  t = 2: -> < 8q;  t = 4: -> < 16q (trivial)
 //   / < 12q;  t = 8: conditional subtract first, -> < 16q.
-template <bool SPQ>
-__device__ __forceinline__ void dit_round3(u64 (&v)[16], const u64* dtw, const Mod<SPQ>& M) {
+template <bool SPQ, bool QA>
+__device__ __forceinline__ void dit_round3(u64 (&v)[16], const u64* dtw, const Mod<SPQ, QA>& M) {
 #pragma unroll
     for (int g = 0; g < 16; g += 2) triv_bfly(v[g], v[g + 1], 2 * M.q);
 #pragma unroll
@@ -303,8 +324,8 @@ __device__ __forceinline__ void dit_round3(u64 (&v)[16], const u64* dtw, const M
 }
 
 // last step of every inverse: x * N^-1 psi^-j (the twist entry f) -> [0, q)
-template <bool SPQ>
-__device__ __forceinline__ u64 twist_out(u64 x, Tw f, const Mod<SPQ>& M) {
+template <bool SPQ, bool QA>
+__device__ __forceinline__ u64 twist_out(u64 x, Tw f, const Mod<SPQ, QA>& M) {
     return canon4m(shoup_lazy(x, f.w, f.wp, M), M);
 }
 
@@ -550,7 +571,7 @@ __global__ __launch_bounds__(256, OFHE_KB_WAVES) void k_block(PlanArgs P, const 
     u64* oblk = dst + off;
     const TowerConst tc = P.tc[t];
     const u64 q = tc.q;
-    const Mod<SPQ> M = load_mod<SPQ>(tc);
+    const auto M = load_mod<SPQ, (bool)OFHE_QA_BLK>(tc);
     const u64* tw = P.tw + (u64)t * N * 2;
     const u32 h = tid >> 4, r = tid & 15;
     // padded LDS bases (lds_pad(p) = p + p/16) of the three round layouts
@@ -770,7 +791,7 @@ __global__ __launch_bounds__(16 * TCOLS_W, OFHE_KB_WAVES) void k_tcols(PlanArgs 
     const u64* x = src + (u64)b * P.sstride + inner;
     u64* y = dst + (u64)b * P.dstride + inner;
     const TowerConst tc = P.tc[t];
-    const Mod<SPQ> M = load_mod<SPQ>(tc);
+    const auto M = load_mod<SPQ, INV ? (bool)OFHE_QA_TCI : (bool)OFHE_QA_TCF>(tc);
     const u32 h = tid / W, r = tid % W;
     const u32 L1 = tid, L2 = h * 16 * W + r;
     u64 v[16];
@@ -1011,7 +1032,7 @@ __global__ __launch_bounds__(256) void k_cols(PlanArgs P, const u64* src, u64* d
     const u64* x = src + (u64)b * P.sstride + inner;
     u64* y = dst + (u64)b * P.dstride + inner;
     const TowerConst tc = P.tc[t];
-    const Mod<SPQ> M = load_mod<SPQ>(tc);
+    const auto M = load_mod<SPQ, INV ? (bool)OFHE_QA_CI : (bool)OFHE_QA_CF>(tc);
     u64 v[CPT][E];
     if (SWS) {
         const u64 w = S.tab[6 * t + 1], wp = S.tab[6 * t + 2];

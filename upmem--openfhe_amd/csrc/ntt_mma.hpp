@@ -63,8 +63,8 @@ __device__ __forceinline__ u32 nm_x(u32 pl, u32 pos) {
 
 // x < 2^(L+4) -> (x mod 2^L) + (x >> L) d < 2^L + 16 d: same residue, small
 // enough for the signed digit split (< 2^63)
-template <bool SPQ>
-__device__ __forceinline__ u64 spq_fold(u64 x, const Mod<SPQ>& M) {
+template <bool SPQ, bool QA>
+__device__ __forceinline__ u64 spq_fold(u64 x, const Mod<SPQ, QA>& M) {
     const u32 qh = hi32(x) >> M.sh;
     const u64 d = (1ull << (M.sh + 32)) - M.q;
     return mad32(qh, lo32(d), pack(lo32(x), hi32(x) & ((1u << M.sh) - 1)));
