@@ -147,6 +147,7 @@ struct ofhe_plan_s {
     // pipeline tuning (ofhe_hip_plan_tune): batch entries per chunk (0 = all)
     // and internal streams the chunks alternate over (1 = caller's stream).
     ofhe::u32 chunk_batch = 0, nstreams = 1;
+    bool chunk_scratch = false;  // chunk intermediates in a reused scratch (OFHE_CHUNK_SCRATCH, A/B)
     bool spq = false;     // every modulus is 2^L - d with d < 2^32 (special-prime kernels)
     // column | block pass split for log_n > 12 (SPLIT_*, ofhe_hip.hip):
     //   SPLIT_COLS  k_cols (log_n - 12 stages) + k_block NR = 3

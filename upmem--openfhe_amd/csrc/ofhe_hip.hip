@@ -328,6 +328,7 @@ int ofhe_hip_plan_create(ofhe_ctx_t ctx, uint32_t log_n, uint32_t towers, const 
     p->spq = true;
     for (u32 t = 0; t < towers; t++) p->spq = p->spq && tc[t].spq_sh != 0;
     if (getenv("OFHE_NO_SPQ")) p->spq = false;  // A/B switch for tests and timing
+    p->chunk_scratch = getenv("OFHE_CHUNK_SCRATCH") != nullptr;
     p->split = split;
     {
         // opt-in (OFHE_NTT_MMA=1): k_block_mma measured 1.7x slower than
@@ -1008,15 +1009,31 @@ int ofhe_hip_ntt_mul_intt(ofhe_plan_t p, const uint64_t* a_, const uint64_t* b, 
             HIPCHK(hipEventRecord(p->ev_fork, s));
             for (int i = 0; i < 2; i++) HIPCHK(hipStreamWaitEvent(p->st[i], p->ev_fork, 0));
         }
+        // OFHE_CHUNK_SCRATCH: each stream's chunks pass their intermediates
+        // through one reused chunk-sized buffer, so those lines are rewritten
+        // in the Infinity Cache instead of landing on fresh addresses of c
+        void* scr[2] = {nullptr, nullptr};
+        const bool use_scr = p->chunk_scratch && cb < batch;
+        for (int i = 0; use_scr && i < (multi ? 2 : 1); i++) {
+            hipStream_t si = multi ? p->st[i] : s;
+            hipError_t e = p->ctx->pool ? hipMallocFromPoolAsync(&scr[i], (size_t)cb * words * 8, p->ctx->pool, si)
+                                        : hipMallocAsync(&scr[i], (size_t)cb * words * 8, si);
+            if (e != hipSuccess) {
+                for (int j = 0; j < i; j++) (void)hipFreeAsync(scr[j], multi ? p->st[j] : s);
+                return fail(OFHE_ERR_NOMEM, std::string("chunk scratch: ") + hipGetErrorString(e));
+            }
+        }
         u32 idx = 0;
         for (u32 b0 = 0; b0 < batch; b0 += cb, idx++) {
             const u32 n = batch - b0 < cb ? batch - b0 : cb;
             hipStream_t sx = multi ? p->st[idx & 1] : s;
             const u64 off = (u64)b0 * words;
-            launch_colpass(a, p->spq, p->split, false, a_ + off, c + off, n, sx);
-            launch_fused_block(p, a, c + off, c + off, b + off, n, sx);
-            launch_colpass(a, p->spq, p->split, true, c + off, c + off, n, sx);
+            u64* mid = use_scr ? (u64*)scr[multi ? (idx & 1) : 0] : c + off;
+            launch_colpass(a, p->spq, p->split, false, a_ + off, mid, n, sx);
+            launch_fused_block(p, a, mid, mid, b + off, n, sx);
+            launch_colpass(a, p->spq, p->split, true, mid, c + off, n, sx);
         }
+        for (int i = 0; use_scr && i < (multi ? 2 : 1); i++) (void)hipFreeAsync(scr[i], multi ? p->st[i] : s);
         if (multi) {
             for (int i = 0; i < 2; i++) {
                 HIPCHK(hipEventRecord(p->ev_join[i], p->st[i]));
