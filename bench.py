@@ -398,6 +398,9 @@ def bench_pipeline(args):
             ok = ok and bool(np.array_equal(cc, O.ntt_mul_intt(aa, bb, tb)))
         parity = ok
 
+    secondary = None
+    if not args.no_extras:
+        secondary = secondary_ops(plan, a, b, c, B, T, n, stream)
     del a, b, c
     torch.cuda.empty_cache()
     extras = {}
@@ -444,6 +447,7 @@ def bench_pipeline(args):
             "parity_spot_check": parity,
             "evalkey_broadcast": bcast,
             "evalkey_broadcast_capi": status,
+            "secondary_ops": secondary,
             "configs3": extras.get("configs3"),
             "keyswitch": extras.get("keyswitch"),
             "rescale": extras.get("rescale"),
@@ -460,6 +464,39 @@ def bench_pipeline(args):
         dist.barrier()
         dist.destroy_process_group()
     return capi_exit_code(status, args.require_capi_comm)
+
+
+def secondary_ops(plan, a, b, c, B, T, n, stream, reps=3):
+    """SURVEY.md §8(d)'s secondary figures at the headline shape, on the same
+    device-resident buffers: the standalone forward / inverse NTT (16
+    algorithmic B per coefficient: read, write) and the vector ModMul / ModAdd
+    (24 B: two reads, one write), HIP events on the launch stream, after the
+    timed region (they leave a and b unchanged: the transforms run on c)."""
+    import torch
+
+    sp = stream.cuda_stream
+    coeffs = B * T * n
+    ops = {
+        "ntt_fwd": (16, lambda: plan.forward(c.data_ptr(), B, sp)),
+        "ntt_inv": (16, lambda: plan.inverse(c.data_ptr(), B, sp)),
+        "modmul": (24, lambda: plan.mod_mul(a.data_ptr(), b.data_ptr(), c.data_ptr(), B, sp)),
+        "modadd": (24, lambda: plan.mod_add(a.data_ptr(), b.data_ptr(), c.data_ptr(), B, sp)),
+    }
+    out = {}
+    for name, (bpc, fn) in ops.items():
+        fn()
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        ev0.record(stream)
+        for _ in range(reps):
+            fn()
+        ev1.record(stream)
+        ev1.synchronize()
+        ms = ev0.elapsed_time(ev1) / reps
+        gbs = bpc * coeffs / (ms * 1e-3) / 1e9
+        out[name] = {"ms": ms, "coeffs_per_s": coeffs / (ms * 1e-3), "alg_bytes_per_coeff": bpc,
+                     "achieved_gbs": gbs, "hbm_frac": gbs / HBM_PEAK_GBS}
+    out["config"] = f"N=2^{n.bit_length() - 1}, towers={T}, batch={B} (the headline buffers)"
+    return out
 
 
 def make_roofline(pipe_ms, kernels_ms, coeffs_rank, log_n, T, B):
