@@ -377,6 +377,7 @@ def bench_pipeline(args):
         kernels_ms[STAGE_NAMES[st]] = ev0.elapsed_time(ev1) / reps
 
     roofline = make_roofline(pipe_ms, kernels_ms, coeffs_rank, log_n, T, B)
+    power = power_sample(step, pipe_ms, local) if (rank == 0 and not args.no_extras) else None
 
     # spot parity check against the oracle (two (batch, tower) rows)
     parity = None
@@ -447,6 +448,7 @@ def bench_pipeline(args):
             "parity_spot_check": parity,
             "evalkey_broadcast": bcast,
             "evalkey_broadcast_capi": status,
+            "power": power,
             "secondary_ops": secondary,
             "configs3": extras.get("configs3"),
             "keyswitch": extras.get("keyswitch"),
@@ -464,6 +466,38 @@ def bench_pipeline(args):
         dist.barrier()
         dist.destroy_process_group()
     return capi_exit_code(status, args.require_capi_comm)
+
+
+def power_sample(step, ms_per_step, device, seconds=2.0):
+    """Package power, power cap and sclk of this rank's GPU while the metric
+    pipeline runs (outside the timed region): ~`seconds` of steps are queued,
+    rocm-smi is read once the firmware has settled, then the queue drains.
+    The pipeline runs at the package power cap on MI355X; the
+    clock the cap allows is what the VALU-bound kernels scale with."""
+    import re
+    import subprocess
+
+    import torch
+
+    n = max(20, int(seconds * 1e3 / max(ms_per_step, 1e-3)))
+    for _ in range(n):
+        step()
+    time.sleep(min(1.0, 0.5 * seconds))
+    try:
+        txt = subprocess.run(["rocm-smi", "-d", str(device), "--showpower", "--showmaxpower", "--showclocks"],
+                             capture_output=True, text=True, timeout=20).stdout
+    except Exception as e:  # no rocm-smi: report why, never fail the bench
+        torch.cuda.synchronize()
+        return {"error": f"{type(e).__name__}: {e}"}
+    torch.cuda.synchronize()
+
+    def num(pat):
+        m = re.search(pat, txt)
+        return float(m.group(1)) if m else None
+
+    return {"package_w": num(r"(?:Current Socket|Average) Graphics Package Power \(W\): ([0-9.]+)"), "cap_w": num(r"Max Graphics Package Power \(W\): ([0-9.]+)"),
+            "sclk_mhz": num(r"sclk clock level: \d+: \((\d+)Mhz\)"), "steps_queued": n,
+            "source": "rocm-smi during ~%.0f s of pipeline steps after the timed region" % seconds}
 
 
 def secondary_ops(plan, a, b, c, B, T, n, stream, reps=3):
