@@ -100,3 +100,25 @@ def test_capi_status_bookkeeping():
     assert st["capi"] is False and st["reasons"] == ["keyswitch: torch.distributed nccl (C-ABI comm: x)"]
     assert bench.capi_exit_code(st, True) == 3 and bench.capi_exit_code(st, False) == 0
     assert bench.capi_exit_code(bench.capi_status({"headline": good}, 2), True) == 0
+
+
+def test_power_sample_parses_rocm_smi(monkeypatch):
+    """bench.power_sample reads the current package power (not the cap, which
+    rocm-smi prints first), the cap and sclk from rocm-smi's text output."""
+    import subprocess
+    import types
+
+    import torch
+
+    import bench
+
+    txt = ("GPU[0]\t\t: sclk clock level: 1: (1946Mhz)\n"
+           "GPU[0]\t\t: Max Graphics Package Power (W): 1400.0\n"
+           "GPU[0]\t\t: Current Socket Graphics Package Power (W): 1391.0\n")
+    monkeypatch.setattr(subprocess, "run", lambda *a, **k: types.SimpleNamespace(stdout=txt))
+    monkeypatch.setattr(torch.cuda, "synchronize", lambda *a, **k: None)
+    monkeypatch.setattr(bench.time, "sleep", lambda s: None)
+    calls = []
+    r = bench.power_sample(lambda: calls.append(1), 10.0, 0, seconds=0.5)
+    assert r["package_w"] == 1391.0 and r["cap_w"] == 1400.0 and r["sclk_mhz"] == 1946.0
+    assert len(calls) == r["steps_queued"] == 50
