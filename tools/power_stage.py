@@ -22,6 +22,9 @@ n = 1 << log_n
 qs, rs = bench.moduli_chain(log_n, T)
 ctx = H.Context(0)
 plan = H.NTTPlan(ctx, log_n, qs, rs)
+if os.environ.get("PS_TUNE"):  # "chunk,streams" for the whole pipeline (ofhe_hip_plan_tune)
+    cb, ns = (int(x) for x in os.environ["PS_TUNE"].split(","))
+    plan.tune(cb, ns)
 s = torch.cuda.current_stream()
 a = torch.empty((B, T, n), dtype=torch.int64, device="cuda")
 b = torch.empty_like(a)
