@@ -9,10 +9,15 @@ range (the generic kernels), and inputs whose words are 0, 1 and q - 1 at
 random positions.  Each case is reproducible from its seed.  The oracle
 follows the reference loops (transformnat-impl.h:300-354, 492-552;
 mubintvecnat.cpp:245-367; dcrtpoly-impl.h:1034-1063)."""
+import os
+
 import numpy as np
 import pytest
 
 from test_gpu_parity import dev, host, stream
+
+# OFHE_FUZZ_SCALE=k multiplies the case counts (a soak run: profiles/r03e_fuzz_soak.txt)
+SCALE = int(os.environ.get("OFHE_FUZZ_SCALE", "1"))
 
 pytestmark = pytest.mark.gpu
 
@@ -56,7 +61,7 @@ def _edge_inputs(rng, B, qs, n):
     return x
 
 
-@pytest.mark.parametrize("seed", range(96))
+@pytest.mark.parametrize("seed", range(96 * SCALE))
 def test_fuzz_plan_ops(hip, O, seed):
     import torch
 
@@ -95,7 +100,7 @@ def test_fuzz_plan_ops(hip, O, seed):
     assert np.array_equal(host(xa), O.ntt_mul_intt(a, b, tb)), "pipeline in place " + ctx_msg
 
 
-@pytest.mark.parametrize("seed", range(48))
+@pytest.mark.parametrize("seed", range(48 * SCALE))
 def test_fuzz_base_conversion(hip, O, seed):
     """ApproxSwitchCRTBasis (dcrtpoly-impl.h:1034-1063) with random source and
     target counts (1 .. 40 sources: the matrix-core kernel's K-step counts
@@ -137,7 +142,7 @@ def _distinct_moduli(O, rng, log_n, count, lo_bits=30):
     return qs, [O.root_of_unity(m, q) for q in qs]
 
 
-@pytest.mark.parametrize("seed", range(48))
+@pytest.mark.parametrize("seed", range(48 * SCALE))
 def test_fuzz_approx_mod_up_down(hip, O, seed):
     """ApproxModUp (dcrtpoly-impl.h:1085-1131, both input forms) and
     ApproxModDown (1134-1175, t = 0 or a random plaintext modulus) on random
