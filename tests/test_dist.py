@@ -55,7 +55,7 @@ def _work(rank, world, port, q):
     try:
         import oracle as O
 
-        log_n, T, GB = 10, 3, 6  # gloo all_gather needs equal shard sizes
+        log_n, T, GB = 10, 3, 3 * world  # gloo all_gather needs equal shard sizes
         n = 1 << log_n
         qs, rs = O.moduli_chain(log_n, T)
         a = O.uniform_dcrt(GB, T, n, qs, 1)
@@ -83,20 +83,23 @@ def _work(rank, world, port, q):
         dist.destroy_process_group()
 
 
-def test_two_rank_shard_and_broadcast():
+@pytest.mark.parametrize("world", [2, 4])
+def test_shard_and_broadcast(world):
+    """world_size 2 (the N > 1 contract) and 4 (a rehearsal of more ranks on
+    gloo): batch shards, the key broadcast and the max-over-ranks timing."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
-    res = [q.get(timeout=120) for _ in procs]
+    res = [q.get(timeout=180) for _ in procs]
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    assert sorted(r[0] for r in res) == [0, 1]
+    assert sorted(r[0] for r in res) == list(range(world))
     assert all(r[1] and r[2] for r in res), res
-    assert all(r[3] == 2.0 for r in res)
+    assert all(r[3] == float(world) for r in res)
 
 
 def _ks_worker(rank, world, port, q):
