@@ -468,7 +468,7 @@ def bench_pipeline(args):
     return capi_exit_code(status, args.require_capi_comm)
 
 
-def power_sample(step, ms_per_step, device, seconds=2.0):
+def power_sample(step, ms_per_step, device, seconds=4.0):
     """Package power, power cap and sclk of this rank's GPU while the metric
     pipeline runs (outside the timed region): ~`seconds` of steps are queued,
     rocm-smi is read once the firmware has settled, then the queue drains.
@@ -482,13 +482,17 @@ def power_sample(step, ms_per_step, device, seconds=2.0):
     n = max(20, int(seconds * 1e3 / max(ms_per_step, 1e-3)))
     for _ in range(n):
         step()
-    time.sleep(min(1.0, 0.5 * seconds))
+    done = torch.cuda.Event()
+    done.record()
+    time.sleep(min(1.5, 0.35 * seconds))
     try:
         txt = subprocess.run(["rocm-smi", "-d", str(device), "--showpower", "--showmaxpower", "--showclocks"],
                              capture_output=True, text=True, timeout=20).stdout
     except Exception as e:  # no rocm-smi: report why, never fail the bench
         torch.cuda.synchronize()
         return {"error": f"{type(e).__name__}: {e}"}
+    # the reading is valid only if the queued steps were still running when it returned
+    busy = not done.query()
     torch.cuda.synchronize()
 
     def num(pat):
@@ -496,7 +500,7 @@ def power_sample(step, ms_per_step, device, seconds=2.0):
         return float(m.group(1)) if m else None
 
     return {"package_w": num(r"(?:Current Socket|Average) Graphics Package Power \(W\): ([0-9.]+)"), "cap_w": num(r"Max Graphics Package Power \(W\): ([0-9.]+)"),
-            "sclk_mhz": num(r"sclk clock level: \d+: \((\d+)Mhz\)"), "steps_queued": n,
+            "sclk_mhz": num(r"sclk clock level: \d+: \((\d+)Mhz\)"), "steps_queued": n, "under_load": busy,
             "source": "rocm-smi during ~%.0f s of pipeline steps after the timed region" % seconds}
 
 

@@ -117,8 +117,10 @@ def test_power_sample_parses_rocm_smi(monkeypatch):
            "GPU[0]\t\t: Current Socket Graphics Package Power (W): 1391.0\n")
     monkeypatch.setattr(subprocess, "run", lambda *a, **k: types.SimpleNamespace(stdout=txt))
     monkeypatch.setattr(torch.cuda, "synchronize", lambda *a, **k: None)
+    monkeypatch.setattr(torch.cuda, "Event", lambda *a, **k: types.SimpleNamespace(record=lambda *a: None,
+                                                                                  query=lambda: False))
     monkeypatch.setattr(bench.time, "sleep", lambda s: None)
     calls = []
     r = bench.power_sample(lambda: calls.append(1), 10.0, 0, seconds=0.5)
-    assert r["package_w"] == 1391.0 and r["cap_w"] == 1400.0 and r["sclk_mhz"] == 1946.0
+    assert r["package_w"] == 1391.0 and r["cap_w"] == 1400.0 and r["sclk_mhz"] == 1946.0 and r["under_load"]
     assert len(calls) == r["steps_queued"] == 50
