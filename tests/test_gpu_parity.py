@@ -474,3 +474,32 @@ def test_block_m16_vs_oracle(hip, O, monkeypatch, T, batch, edge):
     assert np.array_equal(outs[1], O.ntt_mul_intt(a, b, tb))
     bad = np.argwhere(outs[0] != outs[1])
     assert bad.size == 0, (len(bad), bad[:5].tolist())
+
+
+@pytest.mark.parametrize("scratch", [False, True])
+def test_chunked_pipeline_matches(hip, O, scratch, monkeypatch):
+    """ofhe_hip_plan_tune chunking (opt-in A/B settings): chunks of 3 and 4
+    polynomials (a ragged last chunk) on one and two streams, intermediates
+    through c or through the reused chunk scratch (OFHE_CHUNK_SCRATCH), out of
+    place and in place, against the oracle's pipeline."""
+    import torch
+
+    H, ctx = hip
+    log_n, T, B = 16, 3, 7
+    n = 1 << log_n
+    qs, rs = O.moduli_chain(log_n, T)
+    if scratch:
+        monkeypatch.setenv("OFHE_CHUNK_SCRATCH", "1")
+    plan = H.NTTPlan(ctx, log_n, qs, rs)
+    a = O.uniform_dcrt(B, T, n, qs, 71)
+    b = O.uniform_dcrt(B, T, n, qs, 72)
+    want = O.ntt_mul_intt(a, b, O.Tables(n, qs, rs))
+    for cb, ns in ((3, 1), (4, 2), (3, 2)):
+        plan.tune(cb, ns)
+        xa, xb = dev(a), dev(b)
+        xc = torch.empty_like(xa)
+        plan.ntt_mul_intt(xa.data_ptr(), xb.data_ptr(), xc.data_ptr(), B, stream())
+        assert np.array_equal(host(xc), want), (cb, ns)
+        plan.ntt_mul_intt(xa.data_ptr(), xb.data_ptr(), xa.data_ptr(), B, stream())
+        assert np.array_equal(host(xa), want), ("in place", cb, ns)
+    plan.tune(0, 1)
