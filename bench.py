@@ -596,8 +596,12 @@ def make_roofline(pipe_ms, kernels_ms, coeffs_rank, log_n, T, B):
                 "alg_bytes_per_step": alg, "ms_per_step_events": pipe_ms, "valu": valu}
     dominant = max(kernels_ms, key=kernels_ms.get)
     d = kernels[dominant]
-    return {"bound": d["bound"], "achieved": d["achieved_gbs"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
+    # schema 2 (round 3 on): the top-level figures are the dominant kernel's;
+    # round 2's top-level (whole three-launch pipeline) is "pipeline_frac" /
+    # "pipeline", so records stay comparable across rounds
+    return {"schema": 2, "bound": d["bound"], "achieved": d["achieved_gbs"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": d["hbm_frac"], "traffic": d["traffic"], "dominant_kernel": dominant,
+            "pipeline_frac": hbm_frac,
             "scope": f"dominant kernel {dominant}: {KERNEL_BYTES[dominant]} algorithmic B per coefficient x "
                      f"{coeffs_rank} coefficients per launch / its average launch duration (HIP events)",
             "valu": d["valu"], "pipeline": pipeline, "kernels": kernels,

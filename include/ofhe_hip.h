@@ -71,7 +71,10 @@ int ofhe_hip_alloc(ofhe_ctx_t ctx, size_t bytes, void** dptr);
 int ofhe_hip_free(ofhe_ctx_t ctx, void* dptr);
 /* Stream-ordered variants (hipMallocAsync / hipFreeAsync): the block is
  * released only after the work already queued on `stream` has finished, so a
- * buffer can be dropped right after the asynchronous calls that use it. */
+ * buffer can be dropped right after the asynchronous calls that use it.
+ * The blocks come from the context's own pool: ofhe_hip_finalize returns
+ * OFHE_ERR_STATE (and leaves the context usable) while any block obtained
+ * here has not been passed to ofhe_hip_free_async. */
 int ofhe_hip_alloc_async(ofhe_ctx_t ctx, size_t bytes, void** dptr, void* stream);
 int ofhe_hip_free_async(ofhe_ctx_t ctx, void* dptr, void* stream);
 /* Pinned (page-locked) host memory for the staging buffers of a host-buffer

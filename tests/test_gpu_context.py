@@ -1,0 +1,49 @@
+"""GPU tests of the device context's lifetime rules (ofhe_hip_init /
+ofhe_hip_finalize, the PimManager::getPim analogue, PimManager.h:23-29):
+ofhe_hip_alloc_async blocks come from the context's own pool, so finalize must
+refuse while any of them is still allocated (destroying the pool would free
+them under the caller), and succeed once they are freed."""
+import pytest
+
+from test_gpu_parity import stream
+
+pytestmark = pytest.mark.gpu
+
+
+def test_finalize_refused_while_async_blocks_live():
+    import torch
+
+    import ofhe_hip as H
+
+    ctx = H.Context(0)
+    s = stream()
+    p1 = ctx.alloc_async(1 << 20, s)
+    p2 = ctx.alloc_async(4096, s)
+    with pytest.raises(H.MathError, match="still allocated"):
+        ctx.close()
+    # the context is still usable: a block can be written and read back
+    t = torch.arange(512, dtype=torch.int64, device="cuda")
+    ctx.copy_device(p2, t.data_ptr(), 4096, s)
+    back = torch.empty_like(t)
+    ctx.copy_device(back.data_ptr(), p2, 4096, s)
+    torch.cuda.synchronize()
+    assert torch.equal(back, t)
+    ctx.free_async(p1, s)
+    with pytest.raises(H.MathError, match="1 ofhe_hip_alloc_async"):
+        ctx.close()
+    ctx.free_async(p2, s)
+    ctx.free_async(0, s)  # NULL: no-op, not counted
+    torch.cuda.synchronize()
+    ctx.close()
+    with pytest.raises(H.MathError):
+        ctx.alloc_async(64, s)
+
+
+def test_closed_context_rejects_use():
+    import ofhe_hip as H
+
+    ctx = H.Context(0)
+    ctx.close()
+    ctx.close()  # idempotent on the Python side
+    with pytest.raises(H.MathError):
+        _ = ctx.handle

@@ -180,6 +180,40 @@ __device__ __forceinline__ u64 shoup_lazy(u64 a, u64 w, u64 wp, const Mod<SPQ, Q
     return pack(lo32(s), hi);
 }
 
+#ifndef OFHE_ACC_PIN
+#define OFHE_ACC_PIN 1
+#endif
+// acc + shoup_lazy(a, w, wp) mod 2^64 with acc folded into the first
+// multiply-add of the remainder: the Cooley-Tukey butterfly's x + w y costs no
+// separate 64-bit add (the true value acc + [0, 4q) is below 2^64 at every
+// call site, so the wrap-around arithmetic returns it exactly).
+template <bool SPQ, bool QA>
+__device__ __forceinline__ u64 shoup_lazy_acc(u64 a, u64 w, u64 wp, const Mod<SPQ, QA>& M, u64 acc) {
+    const u64 qh = mulhi_approx<QA>(a, wp);
+    u64 s = mad32(lo32(a), lo32(w), acc);
+#if OFHE_ACC_PIN
+    asm("" : "+v"(s));  // keeps LLVM from re-associating acc out of the mad chain
+#endif
+    s = mad32(lo32(qh), lo32(M.nq), s);
+    u32 hi;
+    if (SPQ)
+        hi = hi32(s) + lo32(a) * hi32(w) + hi32(a) * lo32(w) - (lo32(qh) << M.sh) + hi32(qh) * lo32(M.nq);
+    else
+        hi = hi32(s) + lo32(a) * hi32(w) + hi32(a) * lo32(w) + lo32(qh) * hi32(M.nq) + hi32(qh) * lo32(M.nq);
+    return pack(lo32(s), hi);
+}
+
+// Special-prime fold (q = 2^L - d, d < 2^32, 16 d < q; L - 32 = M.sh): any
+// x < 2^(L+4) to r = (x mod 2^L) + (x >> L) d = x - (x >> L) q, r < 2^L + 15 d
+// = q + 16 d < 2q.  Three instructions (shift, mask, one v_mad_u64_u32)
+// against four for a conditional subtract, and a tighter result.
+template <bool SPQ, bool QA>
+__device__ __forceinline__ u64 fold_spq(u64 x, const Mod<SPQ, QA>& M) {
+    const u32 xh = hi32(x) >> M.sh;
+    const u32 d = lo32((1ull << (M.sh + 32)) - M.q);  // wave-uniform (scalar unit)
+    return mad32(xh, d, pack(lo32(x), hi32(x) & ((1u << M.sh) - 1)));
+}
+
 // canonical Shoup: ModMulFastConstEq semantics (result in [0, q)), generic q.
 __device__ __forceinline__ u64 shoup_canon(u64 a, u64 w, u64 wp, u64 q) {
     const Mod<false> M{q, 4 * q, 8 * q, 0 - q, 0 - 4 * q, 0 - 8 * q, 0};

@@ -121,6 +121,7 @@ struct ofhe_ctx_s {
     int device = 0;
     hipMemPool_t pool = nullptr;  // stream-ordered scratch + ofhe_hip_alloc_async (null: the default pool)
     std::atomic<int> live{1};
+    std::atomic<long> async_blocks{0};  // ofhe_hip_alloc_async blocks not yet freed (finalize refuses while > 0)
 };
 
 enum { SPLIT_COLS = 0, SPLIT_T8 = 1, SPLIT_T9 = 2, SPLIT_T8B9 = 3 };
@@ -186,4 +187,8 @@ struct ofhe_bconv_s {
     // calls upload nothing and never synchronise
     std::mutex tab_mu;
     std::map<std::vector<ofhe::u64>, ofhe::u64*> tabs;
+    // k_bconv_cols in ofhe_hip_approx_mod_up / _down: OFHE_BCONV_COLS read when
+    // the converter is created (0: the separate conversion and column-pass
+    // kernels, for A/B runs), as the key-switch engines read it at ks_create
+    bool bcols = true;
 };

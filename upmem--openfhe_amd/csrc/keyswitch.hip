@@ -100,15 +100,6 @@ struct Scratch {
     }
 };
 
-// k_bconv_cols unless OFHE_BCONV_COLS=0 (A/B against the separate kernels)
-bool bcols_default() {
-    static const bool on = [] {
-        const char* e = getenv("OFHE_BCONV_COLS");
-        return !(e && atoi(e) == 0);
-    }();
-    return on;
-}
-
 int copy_rows(u64* dst, u64 dstride, const u64* src, u64 sstride, u64 words, u32 rows, hipStream_t s) {
     if (!words || !rows) return OFHE_OK;
     HIPCHK(hipMemcpy2DAsync(dst, dstride * 8, src, sstride * 8, words * 8, rows, hipMemcpyDeviceToDevice, s));
@@ -231,7 +222,7 @@ int ofhe_hip_approx_mod_up(ofhe_plan_t pq, ofhe_plan_t pp, ofhe_bconv_t bc, int 
         src = out;
         B.in_stride = qp;
     }
-    if (bcols_default() && bconv_cols_ok(pp, B)) {
+    if (bc->bcols && bconv_cols_ok(pp, B)) {
         // the conversion writes the P towers' column-pass output (k_bconv_cols),
         // the block pass finishes their forward transform (1112-1116)
         RCCHK(bconv_cols_run(pp, 0, B, src, out + Q * N, batch, s));
@@ -287,7 +278,7 @@ int ofhe_hip_approx_mod_down(ofhe_plan_t pq, ofhe_plan_t pp, ofhe_bconv_t bc, co
         }
     }
     const TowerScalar* d = (const TowerScalar*)dtab;
-    ModDownArgs A{pq, pp, 0, 0, Q, P, bc->args, d, t ? d + Q : nullptr, t ? d + Q + P : nullptr, bcols_default()};
+    ModDownArgs A{pq, pp, 0, 0, Q, P, bc->args, d, t ? d + Q : nullptr, t ? d + Q + P : nullptr, bc->bcols};
     const u64 N = 1ull << pq->log_n;
     RCCHK(mod_down_run(A, x, (u64)(Q + P) * N, out, (u64)Q * N, batch, s));
     return OFHE_OK;

@@ -169,16 +169,44 @@ __device__ __forceinline__ u64 csub_thr8(u64 x, const Mod<SPQ, QA>& M) {
     const u32 m = (u32)__builtin_amdgcn_sbfe((int)hi32(x), M.sh + 3, 1);
     return x + pack(m & lo32(M.nq8), m & hi32(M.nq8));
 }
+// OFHE_FOLD (special primes): the lazy reductions [0, 16q) -> [0, 8q) (CS
+// stages, GS sums) use fold_spq (3 instructions, result < 2q) instead of the
+// conditional subtract (4).  OFHE_BFLY_ACC: the butterfly's x + w y is the
+// Shoup product with x as the addend of its first multiply-add, and
+// x - w y = (2x + 4q) - (x + w y): one 64-bit add fewer per butterfly.
+#ifndef OFHE_FOLD
+#define OFHE_FOLD 1
+#endif
+#ifndef OFHE_BFLY_ACC
+#define OFHE_BFLY_ACC 1
+#endif
+// [0, 16q) -> [0, 8q) ([0, 2q) by the fold)
+template <bool SPQ, bool QA>
+__device__ __forceinline__ u64 red16(u64 x, const Mod<SPQ, QA>& M) {
+    if (SPQ && OFHE_FOLD) return fold_spq(x, M);
+    return csub_s(x, M.q8);
+}
+// [0, 8q) -> [0, 4q) ([0, 2q) by the fold)
+template <bool SPQ, bool QA>
+__device__ __forceinline__ u64 red8(u64 x, const Mod<SPQ, QA>& M) {
+    if (SPQ && OFHE_FOLD) return fold_spq(x, M);
+    return csub_s(x, M.q4);
+}
 template <bool SPQ, bool QA>
 __device__ __forceinline__ void ct_bfly_cs(u64& x, u64& y, Tw w, const Mod<SPQ, QA>& M, bool cs) {
-    const u64 t = shoup_lazy(y, w.w, w.wp, M);  // [0, 4q)
     u64 a;
     if (OFHE_LAZY_FWD)
-        a = cs ? ((SPQ && OFHE_THR) ? csub_thr8(x, M) : csub_s(x, M.q8)) : x;
+        a = cs ? ((SPQ && OFHE_THR) ? csub_thr8(x, M) : red16(x, M)) : x;
     else
         a = csub_s(x, M.q4);
-    x = a + t;
-    y = a + M.q4 - t;
+    if (OFHE_BFLY_ACC) {
+        x = shoup_lazy_acc(y, w.w, w.wp, M, a);  // a + [0, 4q)
+        y = (a << 1) + M.q4 - x;                 // a + 4q - [0, 4q)
+    } else {
+        const u64 t = shoup_lazy(y, w.w, w.wp, M);  // [0, 4q)
+        x = a + t;
+        y = a + M.q4 - t;
+    }
 }
 template <int CS, class M_>
 __device__ __forceinline__ void ct_bfly(u64& x, u64& y, Tw w, const M_& M) {
@@ -190,7 +218,7 @@ template <class M_>
 __device__ __forceinline__ void gs_bfly(u64& x, u64& y, Tw w, const M_& M) {
     const u64 s = x + y;          // [0, 8q)
     const u64 d = x + M.q4 - y;   // (0, 8q)
-    x = csub_s(s, M.q4);
+    x = red8(s, M);
     y = shoup_lazy(d, w.w, w.wp, M);  // [0, 4q)
 }
 
@@ -314,7 +342,7 @@ __device__ __forceinline__ void dit_round3(u64 (&v)[16], const u64* dtw, const M
         for (int g = 0; g < 16; g += 8) ct_bfly<0>(v[g + j], v[g + j + 4], w, M);
     }
     {
-        const u64 a = csub_s(v[0], M.q8), b = csub_s(v[8], M.q8);
+        const u64 a = red16(v[0], M), b = red16(v[8], M);
         v[0] = a;
         v[8] = b;
         triv_bfly(v[0], v[8], M.q8);
@@ -372,7 +400,7 @@ template <class M_>
 __device__ __forceinline__ void gs_bfly_b(u64& x, u64& y, Tw w, const M_& M, bool in8) {
     const u64 s = x + y;
     const u64 d = x + (in8 ? M.q8 : M.q4) - y;
-    x = in8 ? csub_s(s, M.q8) : s;
+    x = in8 ? red16(s, M) : s;
     y = shoup_lazy(d, w.w, w.wp, M);
 }
 template <int S, class M_>
@@ -629,6 +657,9 @@ __global__ __launch_bounds__(256, OFHE_KB_WAVES) void k_block(PlanArgs P, const 
             for (int k = 0; k < 16; k++) v[k] = canon_fwd<SPQ>(v[k], M);
         }
         if (MODE == MODE_FWD_SUB) {
+            // x + 12q - v needs the forward output v < 12q; OFHE_THR's bit-test
+            // reduction leaves it below 2^(L+3) + 8q (up to 16q), which could wrap
+            static_assert(!OFHE_THR, "the lazy forward-subtract needs the forward output < 12q (OFHE_THR widens it)");
             // (x - NTT(y)) s mod q without canonicalising NTT(y) first: v < 12q
             // (round 3 ends with a CS stage), so d = x + 12q - v is in (0, 13q)
             // < 2^64, the lazy Shoup takes any 64-bit input to [0, 4q), and one

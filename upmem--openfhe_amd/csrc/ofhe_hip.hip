@@ -91,10 +91,18 @@ int ofhe_hip_trim(ofhe_ctx_t ctx, size_t keep_bytes) {
 
 int ofhe_hip_finalize(ofhe_ctx_t ctx) {
     if (!ctx) return fail(OFHE_ERR_ARG, "ctx is NULL");
+    if (ctx->live.load() == 0) return fail(OFHE_ERR_STATE, "context already finalized");
+    // Destroying the pool would release every block still allocated from it,
+    // leaving the caller's ofhe_hip_alloc_async pointers dangling: refuse, and
+    // keep the context usable, until all of them have been freed.
+    const long held = ctx->async_blocks.load();
+    if (held > 0)
+        return fail(OFHE_ERR_STATE, "ofhe_hip_finalize: " + std::to_string(held) +
+                                        " ofhe_hip_alloc_async block(s) still allocated; free them first");
     if (ctx->live.exchange(0) == 0) return fail(OFHE_ERR_STATE, "context already finalized");
     (void)hipSetDevice(ctx->device);
     (void)hipDeviceSynchronize();
-    if (ctx->pool) (void)hipMemPoolDestroy(ctx->pool);  // blocks still allocated from it are released with it
+    if (ctx->pool) (void)hipMemPoolDestroy(ctx->pool);  // only the library's own (freed) scratch is left in it
     delete ctx;
     return OFHE_OK;
 }
@@ -121,6 +129,7 @@ int ofhe_hip_alloc_async(ofhe_ctx_t ctx, size_t bytes, void** dptr, void* stream
     hipError_t e = ctx->pool ? hipMallocFromPoolAsync(dptr, bytes ? bytes : 1, ctx->pool, pick(stream))
                              : hipMallocAsync(dptr, bytes ? bytes : 1, pick(stream));
     if (e != hipSuccess) return fail(OFHE_ERR_NOMEM, std::string("hipMallocAsync: ") + hipGetErrorString(e));
+    ctx->async_blocks.fetch_add(1);
     return OFHE_OK;
 }
 
@@ -129,6 +138,7 @@ int ofhe_hip_free_async(ofhe_ctx_t ctx, void* dptr, void* stream) {
     if (!dptr) return OFHE_OK;
     HIPCHK(hipSetDevice(ctx->device));
     HIPCHK(hipFreeAsync(dptr, pick(stream)));
+    ctx->async_blocks.fetch_sub(1);
     return OFHE_OK;
 }
 
@@ -1324,6 +1334,10 @@ int ofhe_hip_bconv_create(ofhe_ctx_t ctx, uint32_t log_n, uint32_t size_q, uint3
     ofhe_bconv_s* b = new (std::nothrow) ofhe_bconv_s();
     if (!b) return fail(OFHE_ERR_NOMEM, "bconv allocation failed");
     b->ctx = ctx;
+    {
+        const char* e = getenv("OFHE_BCONV_COLS");
+        b->bcols = !(e && atoi(e) == 0);
+    }
     hipError_t e = hipSetDevice(ctx->device);
     if (e == hipSuccess) e = hipMalloc(&b->d_mem, words_all * sizeof(u64));
     if (e == hipSuccess) e = upload_blocking(b->d_mem, h.data(), words_all * sizeof(u64));

@@ -95,8 +95,12 @@ public:
         sync();
     }
     void sync() { check(ofhe_hip_sync(ctx_, nullptr), "HipManager::sync"); }
+    // ofhe_hip_finalize refuses (OFHE_ERR_STATE) while DeviceBuffers still
+    // hold blocks of the context's pool: the context is then left alive for
+    // them (they free through the context handle, not through this object),
+    // and process exit reclaims it.
     ~HipManager() {
-        if (ctx_) ofhe_hip_finalize(ctx_);
+        if (ctx_) (void)ofhe_hip_finalize(ctx_);
     }
     HipManager(const HipManager&) = delete;
     HipManager& operator=(const HipManager&) = delete;
@@ -111,7 +115,7 @@ private:
 class DeviceBuffer {
 public:
     DeviceBuffer() = default;
-    DeviceBuffer(HipManager* m, size_t words) : m_(m), n_(words) {
+    DeviceBuffer(HipManager* m, size_t words) : m_(m), ctx_(m->ctx()), n_(words) {
         if (words) p_ = static_cast<uint64_t*>(m_->allocate(words * sizeof(uint64_t)));
     }
     DeviceBuffer(const DeviceBuffer&) = delete;
@@ -122,7 +126,7 @@ public:
         return *this;
     }
     ~DeviceBuffer() {
-        if (p_) (void)ofhe_hip_free_async(m_->ctx(), p_, nullptr);  // stream-ordered, no wait
+        if (p_) (void)ofhe_hip_free_async(ctx_, p_, nullptr);  // stream-ordered, no wait
     }
     uint64_t* get() const { return p_; }
     size_t size() const { return n_; }
@@ -136,10 +140,12 @@ public:
 private:
     void swap(DeviceBuffer& o) {
         std::swap(m_, o.m_);
+        std::swap(ctx_, o.ctx_);
         std::swap(p_, o.p_);
         std::swap(n_, o.n_);
     }
     HipManager* m_ = nullptr;
+    ofhe_ctx_t ctx_ = nullptr;
     uint64_t* p_ = nullptr;
     size_t n_ = 0;
 };
