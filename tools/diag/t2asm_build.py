@@ -45,6 +45,9 @@ untracked build output) and writes the variants:
   vgpr64    the unchanged code with its VGPR allocation raised from 56 to 64
             (next_free_vgpr / accum_offset / metadata only)
   vgpr48x   every wave's allocation 56 -> 72 (above 64: 7 waves per SIMD)
+  vgprN     the same with the allocation raised to N = 80, 88, ..., 128
+            (round 4: the sweep of every granule up to 128, 4+ waves per SIMD,
+            so two or more 256-thread workgroups share each CU)
   dumpin    out0 receives the c1 pair as loaded (v[14:17], stored right after
             the first s_waitcnt that covers its load, through v[56:57]) and
             keeps nothing else: the kernel's own view of its inputs
@@ -108,8 +111,8 @@ def variant(text, kind):
         return nobranch(text)
     if kind == "nont":
         return text.replace(", off nt", ", off")
-    if kind in ("vgpr64", "vgpr48x"):
-        n = 64 if kind == "vgpr64" else 72
+    if kind in ("vgpr64", "vgpr48x") or re.fullmatch(r"vgpr\d+", kind):
+        n = 64 if kind == "vgpr64" else 72 if kind == "vgpr48x" else int(kind[4:])
         text = text.replace(".amdhsa_next_free_vgpr 56", ".amdhsa_next_free_vgpr %d" % n)
         text = text.replace(".amdhsa_accum_offset 56", ".amdhsa_accum_offset %d" % n)
         return re.sub(r"(\.vgpr_count:\s+)56", r"\g<1>%d" % n, text)
@@ -167,7 +170,14 @@ def main():
     if src:
         open(orig, "w").write(extract(src))
     text = open(orig).read()
-    for kind in ("orig", "nop", "carry", "endwait", "zero", "execnop", "nobranch", "vnop", "rcpnop", "allnop", "nont", "vmwait", "dump", "dumpin", "vgpr64", "vgpr48x"):
+    kinds = ["orig", "nop", "carry", "endwait", "zero", "execnop", "nobranch", "vnop", "rcpnop", "allnop", "nont",
+             "vmwait", "dump", "dumpin", "vgpr64", "vgpr48x"]
+    # round 4: the same machine code at every allocation from 64
+    # to 128 VGPRs (granule 8), each run with two or more workgroups per CU
+    kinds += ["vgpr%d" % n for n in range(80, 129, 8)]
+    if os.environ.get("T2_KINDS"):
+        kinds = os.environ["T2_KINDS"].split(",")
+    for kind in kinds:
         s = os.path.join(HERE, f"t2_{kind}_gen.s")
         o = os.path.join(HERE, f"t2_{kind}.o")
         co = os.path.join(HERE, f"t2_{kind}.hsaco")

@@ -187,10 +187,15 @@ static long run(hipFunction_t fn, const char* name, u32 log_n, u32 towers, u32 b
 int main(int argc, char** argv) {
     const std::string dir = argc > 1 ? argv[1] : ".";
     const char* kname = "_ZN4ofhe9k_tensor2ILi0EEEvPKNS_10TowerConstEPKmS5_S5_S5_PmS6_S6_mjj";
-    const char* kinds[] = {"vgpr64", "vgpr48x", "orig", "dumpin", "dump", "allnop", "nont", "vmwait", "rcpnop", "nobranch", "vnop", "endwait", "zero",
+    const char* kinds_all[] = {"vgpr64", "vgpr48x", "orig", "dumpin", "dump", "allnop", "nont", "vmwait", "rcpnop", "nobranch", "vnop", "endwait", "zero",
                            "execnop", "nop", "carry"};
+    // T2_SWEEP (round 4): the allocation sweep, 56 (orig) .. 128 VGPRs
+    const char* kinds_sweep[] = {"orig", "vgpr64", "vgpr48x", "vgpr80", "vgpr88", "vgpr96", "vgpr104", "vgpr112", "vgpr120", "vgpr128"};
+    const bool sweep = getenv("T2_SWEEP") != nullptr;
+    const char** kinds = sweep ? kinds_sweep : kinds_all;
+    const int nall = sweep ? (int)(sizeof(kinds_sweep) / sizeof(kinds_sweep[0])) : (int)(sizeof(kinds_all) / sizeof(kinds_all[0]));
     const int only = getenv("T2_ONLY") ? atoi(getenv("T2_ONLY")) : 99;
-    const int nk = only < 99 ? only : (int)(sizeof(kinds) / sizeof(kinds[0]));
+    const int nk = only < 99 ? only : nall;
     long bad[16] = {};
     for (int v = 0; v < nk; v++) {
         hipModule_t m;

@@ -25,6 +25,10 @@ if [ -z "$SKIP_AB" ]; then
         EXP_ROUNDS=${EXP_KS_ROUNDS:-6} step exp_ks 300 python -u tools/exp_ks.py || exit $?
     fi
 fi
+if [ -n "$RUN_DIAG" ]; then
+    # VGPR-allocation sweep of the round-2 EvalMultCore machine code
+    T2_SWEEP=1 step vgpr_sweep 180 tools/diag/tensor2_asm_diag_bin tools/diag || exit $?
+fi
 if [ -n "$RUN_BENCH" ]; then
     step bench 400 python -u bench.py ${BENCH_ARGS} || exit $?
 fi
