@@ -186,11 +186,23 @@ __device__ __forceinline__ u64 red16(u64 x, const Mod<SPQ, QA>& M) {
     if (SPQ && OFHE_FOLD) return fold_spq(x, M);
     return csub_s(x, M.q8);
 }
+// The Gentleman-Sande sums keep the conditional subtract by default
+// (OFHE_FOLD_GS=0): same-process A/B, the inverse column pass was 1 % slower
+// with the fold there (profiles/r04a_fold_acc_ab.txt, r04b_qh2_ab.txt).
+#ifndef OFHE_FOLD_GS
+#define OFHE_FOLD_GS 0
+#endif
 // [0, 8q) -> [0, 4q) ([0, 2q) by the fold)
 template <bool SPQ, bool QA>
 __device__ __forceinline__ u64 red8(u64 x, const Mod<SPQ, QA>& M) {
-    if (SPQ && OFHE_FOLD) return fold_spq(x, M);
+    if (SPQ && OFHE_FOLD && OFHE_FOLD_GS) return fold_spq(x, M);
     return csub_s(x, M.q4);
+}
+// GS sums [0, 16q) -> [0, 8q)
+template <bool SPQ, bool QA>
+__device__ __forceinline__ u64 red16_gs(u64 x, const Mod<SPQ, QA>& M) {
+    if (SPQ && OFHE_FOLD && OFHE_FOLD_GS) return fold_spq(x, M);
+    return csub_s(x, M.q8);
 }
 template <bool SPQ, bool QA>
 __device__ __forceinline__ void ct_bfly_cs(u64& x, u64& y, Tw w, const Mod<SPQ, QA>& M, bool cs) {
@@ -199,7 +211,11 @@ __device__ __forceinline__ void ct_bfly_cs(u64& x, u64& y, Tw w, const Mod<SPQ, 
         a = cs ? ((SPQ && OFHE_THR) ? csub_thr8(x, M) : red16(x, M)) : x;
     else
         a = csub_s(x, M.q4);
-    if (OFHE_BFLY_ACC) {
+    if (OFHE_BFLY_ACC == 2) {
+        const u64 c2 = (a << 1) + M.q4;          // computed first: a dies in the mad chain
+        x = shoup_lazy_acc(y, w.w, w.wp, M, a);  // a + [0, 4q)
+        y = c2 - x;                              // a + 4q - [0, 4q)
+    } else if (OFHE_BFLY_ACC) {
         x = shoup_lazy_acc(y, w.w, w.wp, M, a);  // a + [0, 4q)
         y = (a << 1) + M.q4 - x;                 // a + 4q - [0, 4q)
     } else {
@@ -400,7 +416,7 @@ template <class M_>
 __device__ __forceinline__ void gs_bfly_b(u64& x, u64& y, Tw w, const M_& M, bool in8) {
     const u64 s = x + y;
     const u64 d = x + (in8 ? M.q8 : M.q4) - y;
-    x = in8 ? red16(s, M) : s;
+    x = in8 ? red16_gs(s, M) : s;
     y = shoup_lazy(d, w.w, w.wp, M);
 }
 template <int S, class M_>
