@@ -112,6 +112,21 @@ int ofhe_hip_plan_destroy(ofhe_plan_t plan);
  * joined back into the caller's stream.  Results are identical for any
  * setting; only speed changes. */
 int ofhe_hip_plan_tune(ofhe_plan_t plan, uint32_t chunk_batch, uint32_t streams);
+/* Performance knob for ofhe_hip_ntt_mul_intt at log_n = 16 (the SwitchFormat ->
+ * Times -> SwitchFormat chain of dcrtpoly-impl.h:2518-2524 / dcrtpoly.h:185-200):
+ * persistent = 1 runs the three passes as one persistent launch whose XCDs
+ * each drain a software-pipelined queue of (pass, tower) work items, lag =
+ * steps between a tower's passes (0 = default); persistent = 0 restores the
+ * three launches.  Fails with OFHE_ERR_STATE when the plan cannot run it
+ * (log_n != 16, or the device's workgroup placement did not pass the plan's
+ * one-time XCD probe).  Chunking (ofhe_hip_plan_tune) takes precedence.
+ * Results are identical either way. */
+int ofhe_hip_plan_pipeline(ofhe_plan_t plan, int persistent, uint32_t lag);
+/* Whether the persistent pipeline is selected, and how many of its waits gave
+ * up since the plan was created (0 unless an invariant broke; the outputs of
+ * such a call are not to be trusted).  Synchronises the device.  No
+ * reference counterpart (diagnostics of ofhe_hip_plan_pipeline). */
+int ofhe_hip_plan_pipeline_status(ofhe_plan_t plan, int* persistent, uint32_t* faults);
 /* Copy the plan's host-side tables out (debug / parity tests): any pointer
  * may be NULL.  tab*: [towers][N] in OpenFHE order (Table[rev(i)] = psi^i). */
 int ofhe_hip_plan_tables(ofhe_plan_t plan, uint64_t* tab, uint64_t* tab_pre, uint64_t* itab,

@@ -149,6 +149,13 @@ struct ofhe_plan_s {
     // and internal streams the chunks alternate over (1 = caller's stream).
     ofhe::u32 chunk_batch = 0, nstreams = 1;
     bool chunk_scratch = false;  // chunk intermediates in a reused scratch (OFHE_CHUNK_SCRATCH, A/B)
+    // persistent pipeline (k_pipe, pipe_kernels.hpp; ofhe_hip_plan_pipeline):
+    // selected, lag, grid, and the one-time XCD probe (0 not run, 1 passed,
+    // -1 failed / not applicable); d_pipe_err counts given-up waits
+    bool pipe = false;
+    ofhe::u32 pipe_lag = 4, pipe_grid = 0, pipe_nq = 8;
+    int pipe_state = 0;
+    ofhe::u32* d_pipe_err = nullptr;
     bool spq = false;     // every modulus is 2^L - d with d < 2^32 (special-prime kernels)
     // column | block pass split for log_n > 12 (SPLIT_*, ofhe_hip.hip):
     //   SPLIT_COLS  k_cols (log_n - 12 stages) + k_block NR = 3

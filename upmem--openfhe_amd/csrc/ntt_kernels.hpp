@@ -120,6 +120,16 @@ __device__ __forceinline__ void st_s(u64* p, u64 v) {
     else
         *p = v;
 }
+// streaming (NT = true, as ld_s / st_s) or cached access, chosen per call site
+template <bool NT>
+__device__ __forceinline__ u64 ld_m(const u64* p) { return NT ? ld_s(p) : *p; }
+template <bool NT>
+__device__ __forceinline__ void st_m(u64* p, u64 v) {
+    if (NT)
+        st_s(p, v);
+    else
+        *p = v;
+}
 __device__ __forceinline__ u64x2 ld2_s(const u64* p) {
     const u64x2* q = reinterpret_cast<const u64x2*>(p);
     return OFHE_NT ? __builtin_nontemporal_load(q) : *q;
@@ -593,18 +603,19 @@ __device__ __forceinline__ void wave_stage_out(const u64 (&v)[16], u64* lds, u32
 // stages of round 1 (strides 2048, 1024, 512), so the forward round 1 keeps
 // its last stage (stride 256) and the inverse round 1' its first (t = 256);
 // the inverse twist is the one of 512-element groups.
-template <int MODE, bool SPQ, int NR, int SK = 0>
-__global__ __launch_bounds__(256, OFHE_KB_WAVES) void k_block(PlanArgs P, const u64* src, u64* dst,
-                                                              const u64* __restrict__ bdat, u32 batch, u32 nwg) {
-    OFHE_VGPR_FLOOR();
+// The body of k_block for work item wid (block g = wid % G of polynomial
+// tower pb = wid / G), on the caller's LDS (LDS_WORDS words).  IM: bit 0 =
+// the input is an intermediate another pass of the same launch wrote (cached
+// loads), bit 1 = the output is one (cached stores) -- k_pipe; 0 streams both.
+template <int MODE, bool SPQ, int NR, int SK = 0, int IM = 0>
+__device__ __forceinline__ void block_body(const PlanArgs& P, const u64* src, u64* dst, const u64* __restrict__ bdat,
+                                           u32 batch, u32 wid, u64* lds, u32 tid) {
     static_assert(NR == 2 || NR == 3, "k_block covers the last 8 (NR=2) or 12 (NR=3) stages");
     static_assert(SK == 0 || (SK == 3 && NR == 3), "k_block: SK = 3 needs NR = 3");
-    __shared__ u64 lds[LDS_WORDS];
-    const u32 tid = threadIdx.x;
+    constexpr bool NTI = !(IM & 1), NTO = !(IM & 2);
     const u32 logn = P.log_n;
     const u32 N = 1u << logn;
     const u32 G = N >> 12;  // blocks per polynomial
-    const u32 wid = xcd_remap(blockIdx.x, nwg);
     const u32 g = wid % G;
     const u32 pb = wid / G;
     const u32 t = pb / batch, b = pb % batch;
@@ -628,7 +639,7 @@ __global__ __launch_bounds__(256, OFHE_KB_WAVES) void k_block(PlanArgs P, const 
         if (NR == 3) {
             // round 1: st = 256, p = tid + 256k
 #pragma unroll
-            for (int k = 0; k < 16; k++) v[k] = ld_s(blk + tid + 256 * k);
+            for (int k = 0; k < 16; k++) v[k] = ld_m<NTI>(blk + tid + 256 * k);
             if (SK == 3)
                 fwd_stage16<3>(v, tw, (N >> 12) + g, M);  // input < 12q (k_tcols) -> < 12q
             else
@@ -641,7 +652,7 @@ __global__ __launch_bounds__(256, OFHE_KB_WAVES) void k_block(PlanArgs P, const 
             for (int k = 0; k < 16; k++) v[k] = lds[L2 + 17 * k];
         } else {
 #pragma unroll
-            for (int k = 0; k < 16; k++) v[k] = ld_s(blk + h * 256 + r + 16 * k);
+            for (int k = 0; k < 16; k++) v[k] = ld_m<NTI>(blk + h * 256 + r + 16 * k);
         }
         fwd_round16(v, tw, (N >> 8) + g * 16 + h, M);
 #pragma unroll
@@ -758,7 +769,7 @@ __global__ __launch_bounds__(256, OFHE_KB_WAVES) void k_block(PlanArgs P, const 
         for (int k = 0; k < 16; k++) {
             const u32 p = h * 256 + r + 16 * k;
             const Tw f = ldtw(tw_, p);
-            st_s(oblk + p, shoup_lazy(v[k], f.w, f.wp, M));
+            st_m<NTO>(oblk + p, shoup_lazy(v[k], f.w, f.wp, M));
         }
         return;
     }
@@ -777,7 +788,14 @@ __global__ __launch_bounds__(256, OFHE_KB_WAVES) void k_block(PlanArgs P, const 
         v[k] = logn == 12 ? twist_out(v[k], f, M) : shoup_lazy(v[k], f.w, f.wp, M);
     }
 #pragma unroll
-    for (int k = 0; k < 16; k++) st_s(oblk + tid + 256 * k, v[k]);
+    for (int k = 0; k < 16; k++) st_m<NTO>(oblk + tid + 256 * k, v[k]);
+}
+template <int MODE, bool SPQ, int NR, int SK = 0>
+__global__ __launch_bounds__(256, OFHE_KB_WAVES) void k_block(PlanArgs P, const u64* src, u64* dst,
+                                                              const u64* __restrict__ bdat, u32 batch, u32 nwg) {
+    OFHE_VGPR_FLOOR();
+    __shared__ u64 lds[LDS_WORDS];
+    block_body<MODE, SPQ, NR, SK>(P, src, dst, bdat, batch, xcd_remap(blockIdx.x, nwg), lds, threadIdx.x);
 }
 
 // Rescaling source of the forward column pass (k_cols / k_tcols <.., SWS = true>):
@@ -814,11 +832,15 @@ static_assert(TCOLS_W == 16 || TCOLS_W == 32, "column tile width");
 // LOGN = 17 (the 8 | 9 split, SPLIT_T8B9): element j = row * 512 + col, the
 // same 256-row sub-transforms on 512 columns (the twiddle index of stage m is
 // m + row / (256 / m) whatever the row length).
-template <bool INV, bool SPQ, bool SWS = false, int LOGN = 16>
-__global__ __launch_bounds__(16 * TCOLS_W, OFHE_KB_WAVES) void k_tcols(PlanArgs P, const u64* src, u64* dst,
-                                                                       u32 batch, u32 nwg, SwSrc SWA) {
-    OFHE_VGPR_FLOOR();
+constexpr u32 TCOLS_LDS_WORDS = 16 * 16 * TCOLS_W + 16 * 16;
+// The body of k_tcols for work item wid (column tile cb = wid % (S / W) of
+// polynomial tower pb = wid / (S / W)) on the caller's LDS (TCOLS_LDS_WORDS);
+// IM as block_body's.
+template <bool INV, bool SPQ, bool SWS = false, int LOGN = 16, int IM = 0>
+__device__ __forceinline__ void tcols_body(const PlanArgs& P, const u64* src, u64* dst, u32 batch, u32 wid,
+                                           const SwSrc& SWA, u64* lds, u32 tid) {
     static_assert(LOGN == 16 || LOGN == 17, "k_tcols: N = 2^16 or 2^17");
+    constexpr bool NTI = !(IM & 1), NTO = !(IM & 2);
     constexpr u32 N = 1u << LOGN, S = N / 256, W = TCOLS_W;
     // Exchange patterns p = tid + 16W k (round 1) and p = 16W h + W k + r
     // (round 2).  The inverse writes the second and reads the first: unpadded,
@@ -828,9 +850,6 @@ __global__ __launch_bounds__(16 * TCOLS_W, OFHE_KB_WAVES) void k_tcols(PlanArgs 
     // banks (2-way, measured 0.56 conflict cycles per active LDS cycle); with
     // OFHE_TCOLS_PADF it shifts row h by 16 words per 16W-word row
     // (lds index p + 16 (p / 16W)), so rows h and h + 1 cover all 64 banks.
-    __shared__ u64 lds[16 * 16 * W + 16 * 16];
-    const u32 tid = threadIdx.x;
-    const u32 wid = xcd_remap(blockIdx.x, nwg);
     const u32 cb = wid % (S / W);
     const u32 pb = wid / (S / W);
     const u32 t = pb / batch, b = pb % batch;
@@ -859,7 +878,7 @@ __global__ __launch_bounds__(16 * TCOLS_W, OFHE_KB_WAVES) void k_tcols(PlanArgs 
             }
         } else {
 #pragma unroll
-            for (int k = 0; k < 16; k++) v[k] = ld_s(x + (u64)(h + 16 * k) * S + r);
+            for (int k = 0; k < 16; k++) v[k] = ld_m<NTI>(x + (u64)(h + 16 * k) * S + r);
         }
         fwd_round16_canon(v, tw, 1, M);
 #pragma unroll
@@ -870,11 +889,11 @@ __global__ __launch_bounds__(16 * TCOLS_W, OFHE_KB_WAVES) void k_tcols(PlanArgs 
         for (int k = 0; k < 16; k++) v[k] = lds[h * RP + r + W * k];
         fwd_round16(v, tw, 16 + h, M);
 #pragma unroll
-        for (int k = 0; k < 16; k++) st_s(y + (u64)(16 * h + k) * S + r, v[k]);
+        for (int k = 0; k < 16; k++) st_m<NTO>(y + (u64)(16 * h + k) * S + r, v[k]);
     } else {
         const u64* itw = P.itw + (u64)t * N * 2;
 #pragma unroll
-        for (int k = 0; k < 16; k++) v[k] = ld_s(x + (u64)(16 * h + k) * S + r);
+        for (int k = 0; k < 16; k++) v[k] = ld_m<NTI>(x + (u64)(16 * h + k) * S + r);
         if (OFHE_LAZY_GS) {
             // input < 4q (the block pass's lazy twist); round 2's registers all
             // come from one round-1 position, taken as < 8q
@@ -893,7 +912,7 @@ __global__ __launch_bounds__(16 * TCOLS_W, OFHE_KB_WAVES) void k_tcols(PlanArgs 
             inv_round16_b(v, b8, itw, 1, M);
 #pragma unroll
             for (int k = 0; k < 16; k++)
-                st_s(y + (u64)(h + 16 * k) * S + r, b8[k] ? canon8m(v[k], M) : canon4m(v[k], M));
+                st_m<NTO>(y + (u64)(h + 16 * k) * S + r, b8[k] ? canon8m(v[k], M) : canon4m(v[k], M));
         } else {
             inv_round16(v, itw, 16 + h, M);
 #pragma unroll
@@ -903,9 +922,17 @@ __global__ __launch_bounds__(16 * TCOLS_W, OFHE_KB_WAVES) void k_tcols(PlanArgs 
             for (int k = 0; k < 16; k++) v[k] = lds[L1 + 16 * W * k];
             inv_round16(v, itw, 1, M);
 #pragma unroll
-            for (int k = 0; k < 16; k++) st_s(y + (u64)(h + 16 * k) * S + r, canon4m(v[k], M));
+            for (int k = 0; k < 16; k++) st_m<NTO>(y + (u64)(h + 16 * k) * S + r, canon4m(v[k], M));
         }
     }
+}
+
+template <bool INV, bool SPQ, bool SWS = false, int LOGN = 16>
+__global__ __launch_bounds__(16 * TCOLS_W, OFHE_KB_WAVES) void k_tcols(PlanArgs P, const u64* src, u64* dst,
+                                                                       u32 batch, u32 nwg, SwSrc SWA) {
+    OFHE_VGPR_FLOOR();
+    __shared__ u64 lds[TCOLS_LDS_WORDS];
+    tcols_body<INV, SPQ, SWS, LOGN>(P, src, dst, batch, xcd_remap(blockIdx.x, nwg), SWA, lds, threadIdx.x);
 }
 
 // ---------------------------------------------------------------------------

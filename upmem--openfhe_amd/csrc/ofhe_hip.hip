@@ -20,6 +20,7 @@
 #include "ntt_mma.hpp"
 #include "ntt_m16.hpp"
 #include "bconv_cols.hpp"
+#include "pipe_kernels.hpp"
 
 using namespace ofhe;
 
@@ -407,6 +408,75 @@ int ofhe_hip_plan_tune(ofhe_plan_t p, uint32_t chunk_batch, uint32_t streams) {
     return OFHE_OK;
 }
 
+// One-time check that k_pipe's queues map one-to-one onto XCDs: a grid of
+// k_pipe's size records the XCD of every workgroup, and all of 0 .. nq - 1
+// must occur and nothing else (SPX mode).  Synchronises; runs on the first
+// ofhe_hip_plan_pipeline(persistent = 1) only.
+static int pipe_probe(ofhe_plan_t p) {
+    int occ = 0, ncu = 0;
+    HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(
+        &occ, p->spq ? (const void*)k_pipe<true> : (const void*)k_pipe<false>, 256, 0));
+    HIPCHK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, p->ctx->device));
+    if (occ < 1 || ncu < 1) return fail(OFHE_ERR_STATE, "persistent pipeline: kernel does not fit a CU");
+    const u32 grid = (u32)occ * (u32)ncu;
+    u32* d = nullptr;
+    HIPCHK(hipMalloc(&d, sizeof(u32) * grid));
+    hipLaunchKernelGGL(k_pipe_probe, dim3(grid), dim3(256), 0, nullptr, d);
+    std::vector<u32> x(grid);
+    hipError_t e = hipGetLastError();
+    if (e == hipSuccess) e = hipMemcpy(x.data(), d, sizeof(u32) * grid, hipMemcpyDeviceToHost);
+    (void)hipFree(d);
+    if (e != hipSuccess) return fail(OFHE_ERR_HIP, std::string("persistent pipeline probe: ") + hipGetErrorString(e));
+    u32 seen = 0;
+    bool ok = true;
+    for (u32 v : x) {
+        if (v >= p->pipe_nq) ok = false;
+        else seen |= 1u << v;
+    }
+    if (!ok || seen != (1u << p->pipe_nq) - 1) {
+        p->pipe_state = -1;
+        return fail(OFHE_ERR_STATE, "persistent pipeline: workgroups do not map onto 8 XCDs (not SPX mode?)");
+    }
+    HIPCHK(hipMalloc(&p->d_pipe_err, sizeof(u32)));
+    HIPCHK(hipMemset(p->d_pipe_err, 0, sizeof(u32)));
+    HIPCHK(hipDeviceSynchronize());
+    p->pipe_grid = grid;
+    p->pipe_state = 1;
+    return OFHE_OK;
+}
+
+int ofhe_hip_plan_pipeline(ofhe_plan_t p, int persistent, uint32_t lag) {
+    if (!p || !p->ctx) return fail(OFHE_ERR_STATE, "plan is NULL or destroyed");
+    if (lag > 256) return fail(OFHE_ERR_ARG, "lag must be <= 256");
+    HIPCHK(hipSetDevice(p->ctx->device));
+    std::lock_guard<std::mutex> lk(p->fork_mu);
+    if (!persistent) {
+        p->pipe = false;
+        return OFHE_OK;
+    }
+    if (p->log_n != 16 || p->split != SPLIT_T8)
+        return fail(OFHE_ERR_STATE, "persistent pipeline: log_n = 16 plans (8 | 8 pass split) only");
+    if (p->pipe_state == 0) RCCHK(pipe_probe(p));
+    if (p->pipe_state != 1) return fail(OFHE_ERR_STATE, "persistent pipeline: the XCD probe failed on this device");
+    p->pipe_lag = lag ? lag : 4;
+    p->pipe = true;
+    return OFHE_OK;
+}
+
+int ofhe_hip_plan_pipeline_status(ofhe_plan_t p, int* persistent, uint32_t* faults) {
+    if (!p || !p->ctx) return fail(OFHE_ERR_STATE, "plan is NULL or destroyed");
+    if (persistent) *persistent = p->pipe ? 1 : 0;
+    if (faults) {
+        *faults = 0;
+        if (p->d_pipe_err) {
+            HIPCHK(hipSetDevice(p->ctx->device));
+            HIPCHK(hipDeviceSynchronize());
+            HIPCHK(hipMemcpy(faults, p->d_pipe_err, sizeof(u32), hipMemcpyDeviceToHost));
+        }
+    }
+    return OFHE_OK;
+}
+
 int ofhe_hip_plan_destroy(ofhe_plan_t p) {
     if (!p) return fail(OFHE_ERR_ARG, "plan is NULL");
     if (p->ctx) (void)hipSetDevice(p->ctx->device);
@@ -425,6 +495,7 @@ int ofhe_hip_plan_destroy(ofhe_plan_t p) {
     (void)hipFree(p->d_twist_r);
     (void)hipFree(p->d_nm);
     (void)hipFree(p->d_m16);
+    (void)hipFree(p->d_pipe_err);
     for (auto& kv : p->tabs) (void)hipFree(kv.second);
     delete p;
     return OFHE_OK;
@@ -990,6 +1061,36 @@ static void launch_fused_block(ofhe_plan_t p, const PlanArgs& a, const u64* src,
     hipLaunchKernelGGL(k_block_mma, dim3(nwg), dim3(NM_THREADS), 0, s, a, Q, src, dst, b, batch, nwg);
 }
 
+// k_pipe (pipe_kernels.hpp): the three passes as one persistent launch; its
+// queue heads and per-tower counters live in stream-ordered scratch
+static int launch_pipe(ofhe_plan_t p, const PlanArgs& a, const u64* a_, const u64* b, u64* c, u32 batch,
+                       hipStream_t s) {
+    const u64 units = (u64)batch * p->towers;
+    if (units * PIPE_PIECES >= (1ull << 32)) return fail(OFHE_ERR_ARG, "batch too large for the persistent pipeline");
+    const size_t words = (size_t)(p->pipe_nq + 1) * PIPE_QSTRIDE + 2 * units;
+    void* ctl = nullptr;
+    hipError_t e = p->ctx->pool ? hipMallocFromPoolAsync(&ctl, words * 4, p->ctx->pool, s)
+                                : hipMallocAsync(&ctl, words * 4, s);
+    if (e != hipSuccess) return fail(OFHE_ERR_NOMEM, std::string("pipeline counters: ") + hipGetErrorString(e));
+    HIPCHK(hipMemsetAsync(ctl, 0, words * 4, s));
+    PipeCtl C;
+    C.head = (u32*)ctl;
+    C.exited = C.head + (size_t)p->pipe_nq * PIPE_QSTRIDE;
+    C.done_f = C.exited + PIPE_QSTRIDE;
+    C.done_b = C.done_f + units;
+    C.err = p->d_pipe_err;
+    C.units = (u32)units;
+    C.lag = p->pipe_lag;
+    C.nq = p->pipe_nq;
+    if (p->spq)
+        hipLaunchKernelGGL(k_pipe<true>, dim3(p->pipe_grid), dim3(256), 0, s, a, a_, c, b, batch, C);
+    else
+        hipLaunchKernelGGL(k_pipe<false>, dim3(p->pipe_grid), dim3(256), 0, s, a, a_, c, b, batch, C);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipFreeAsync(ctl, s));
+    return post_launch();
+}
+
 int ofhe_hip_ntt_mul_intt(ofhe_plan_t p, const uint64_t* a_, const uint64_t* b, uint64_t* c,
                           uint32_t batch, void* stream) {
     int rc = check_common(p, batch);
@@ -1009,6 +1110,7 @@ int ofhe_hip_ntt_mul_intt(ofhe_plan_t p, const uint64_t* a_, const uint64_t* b, 
         // one chunk's HBM-bound column passes overlap another's VALU-bound
         // block pass.
         const u32 cb = (p->chunk_batch && p->chunk_batch < batch) ? p->chunk_batch : batch;
+        if (p->pipe && cb == batch && !m16_ready(p) && !nm_ready(p)) return launch_pipe(p, a, a_, b, c, batch, s);
         const u64 words = (u64)p->towers << p->log_n;
         const bool multi = p->nstreams == 2 && cb < batch;
         // the fork / join events and side streams are the plan's: one caller at

@@ -65,6 +65,9 @@ _SIGS = {
                                             ctypes.POINTER(_vp)]),
     "ofhe_hip_plan_destroy": (ctypes.c_int, [_vp]),
     "ofhe_hip_plan_tune": (ctypes.c_int, [_vp, ctypes.c_uint32, ctypes.c_uint32]),
+    "ofhe_hip_plan_pipeline": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_uint32]),
+    "ofhe_hip_plan_pipeline_status": (ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_int),
+                                                     ctypes.POINTER(ctypes.c_uint32)]),
     "ofhe_hip_plan_tables": (ctypes.c_int, [_vp, _u64p, _u64p, _u64p, _u64p, _u64p]),
     "ofhe_hip_ntt_fwd": (ctypes.c_int, [_vp, _vp, ctypes.c_uint32, _vp]),
     "ofhe_hip_ntt_inv": (ctypes.c_int, [_vp, _vp, ctypes.c_uint32, _vp]),
@@ -271,6 +274,18 @@ class NTTPlan:
     def tune(self, chunk_batch: int = 0, streams: int = 1) -> None:
         """Chunking / stream knob of ntt_mul_intt (speed only; results are identical)."""
         _check(lib().ofhe_hip_plan_tune(self.handle, int(chunk_batch), int(streams)))
+
+    def pipeline(self, persistent: bool = True, lag: int = 0) -> None:
+        """Select the one-launch persistent ntt_mul_intt pipeline (log_n = 16) or the
+        three launches (speed only; results are identical).  Raises MathError when
+        the plan or the device cannot run it."""
+        _check(lib().ofhe_hip_plan_pipeline(self.handle, 1 if persistent else 0, int(lag)))
+
+    def pipeline_status(self):
+        """(persistent selected, waits given up so far); synchronises the device."""
+        on, faults = ctypes.c_int(), ctypes.c_uint32()
+        _check(lib().ofhe_hip_plan_pipeline_status(self.handle, ctypes.byref(on), ctypes.byref(faults)))
+        return bool(on.value), int(faults.value)
 
     def tables(self):
         """Host copies of (Table, TableP, TableI, TableIP, ninv) as flat lists."""
