@@ -148,6 +148,7 @@ __global__ __launch_bounds__(256, OFHE_KB_WAVES) void k_pipe(PlanArgs P, const u
 
 // one-time placement probe: the XCD of every workgroup of a k_pipe-sized grid
 __global__ void k_pipe_probe(u32* xcc) {
+    OFHE_VGPR_FLOOR();
     if (threadIdx.x == 0) xcc[blockIdx.x] = xcc_id();
 }
 
