@@ -5,7 +5,7 @@
 #   CONFIGS="wg:KiB:passes ..." bash tools/power_l2.sh
 R="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 mkdir -p "$R/gpurun_out"
-OUT="$R/gpurun_out/power_l2.txt"
+OUT="$R/gpurun_out/power_l2_summary.txt"
 : > "$OUT"
 # 1024 wg x 32 KiB = 32 MiB total = 4 MiB per XCD (L2 edge); 512 x 32 = 2 MiB per XCD (L2);
 # 1024 x 128 KiB = 128 MiB (Infinity Cache); 1024 x 4 MiB = 4 GiB (HBM)
