@@ -459,6 +459,17 @@ int ofhe_hip_plan_pipeline(ofhe_plan_t p, int persistent, uint32_t lag) {
     if (p->pipe_state == 0) RCCHK(pipe_probe(p));
     if (p->pipe_state != 1) return fail(OFHE_ERR_STATE, "persistent pipeline: the XCD probe failed on this device");
     p->pipe_lag = lag ? lag : 4;
+    {
+        // OFHE_PIPE_WGS: workgroups per CU (A/B knob: fewer in flight per XCD
+        // means fewer towers' intermediates live in its L2); default: all fit
+        int occ = 0, ncu = 0;
+        HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(
+            &occ, p->spq ? (const void*)k_pipe<true> : (const void*)k_pipe<false>, 256, 0));
+        HIPCHK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, p->ctx->device));
+        const char* w = getenv("OFHE_PIPE_WGS");
+        if (w && atoi(w) > 0 && atoi(w) < occ) occ = atoi(w);
+        p->pipe_grid = (u32)occ * (u32)ncu;
+    }
     p->pipe = true;
     return OFHE_OK;
 }
