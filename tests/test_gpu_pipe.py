@@ -13,11 +13,14 @@ from test_gpu_parity import dev, host, stream
 pytestmark = pytest.mark.gpu
 
 
+@pytest.mark.parametrize("sc1", [False, True])
 @pytest.mark.parametrize("T,B", [(1, 1), (1, 5), (3, 7), (16, 2), (5, 13)])
-def test_pipe_vs_oracle(hip, T, B):
+def test_pipe_vs_oracle(hip, T, B, sc1, monkeypatch):
+    """Both hand-off forms: acquire + plain loads, and sc1 loads (OFHE_PIPE_SC1)."""
     import torch
 
     H, ctx = hip
+    monkeypatch.setenv("OFHE_PIPE_SC1", "1" if sc1 else "0")
     log_n = 16
     n = 1 << log_n
     qs, rs = O.moduli_chain(log_n, T)
@@ -70,13 +73,15 @@ def test_pipe_edge_values_generic_moduli(hip, monkeypatch):
     plan.close()
 
 
-def test_pipe_full_batch_matches_three_launches(hip):
+@pytest.mark.parametrize("sc1", [False, True])
+def test_pipe_full_batch_matches_three_launches(hip, sc1, monkeypatch):
     """configs[2] (N = 2^16, 16 towers, batch 1024, 8 GiB per operand): the
     persistent pipeline's c equals the three-launch pipeline's, every word, and
     sampled rows equal the oracle."""
     import torch
 
     H, ctx = hip
+    monkeypatch.setenv("OFHE_PIPE_SC1", "1" if sc1 else "0")
     log_n, T, B = 16, 16, 1024
     n = 1 << log_n
     qs, rs = O.moduli_chain(log_n, T)

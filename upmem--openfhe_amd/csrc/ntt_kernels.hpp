@@ -120,9 +120,15 @@ __device__ __forceinline__ void st_s(u64* p, u64 v) {
     else
         *p = v;
 }
-// streaming (NT = true, as ld_s / st_s) or cached access, chosen per call site
-template <bool NT>
-__device__ __forceinline__ u64 ld_m(const u64* p) { return NT ? ld_s(p) : *p; }
+// streaming (NT = true, as ld_s / st_s) or cached access, chosen per call site;
+// ld_m<LD_SC1> loads with sc1 (served by the XCD's L2, bypassing the CU's L1:
+// data another CU of the same XCD stored in this launch, k_pipe)
+enum { LD_PLAIN = 0, LD_NT = 1, LD_SC1 = 2 };
+template <int LD>
+__device__ __forceinline__ u64 ld_m(const u64* p) {
+    if (LD == LD_SC1) return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return LD == LD_NT ? ld_s(p) : *p;
+}
 template <bool NT>
 __device__ __forceinline__ void st_m(u64* p, u64 v) {
     if (NT)
@@ -606,13 +612,15 @@ __device__ __forceinline__ void wave_stage_out(const u64 (&v)[16], u64* lds, u32
 // The body of k_block for work item wid (block g = wid % G of polynomial
 // tower pb = wid / G), on the caller's LDS (LDS_WORDS words).  IM: bit 0 =
 // the input is an intermediate another pass of the same launch wrote (cached
-// loads), bit 1 = the output is one (cached stores) -- k_pipe; 0 streams both.
+// loads), bit 1 = the output is one (cached stores), bit 2 = load that input
+// with sc1 (L1 bypass, no acquire needed) -- k_pipe; 0 streams both.
 template <int MODE, bool SPQ, int NR, int SK = 0, int IM = 0>
 __device__ __forceinline__ void block_body(const PlanArgs& P, const u64* src, u64* dst, const u64* __restrict__ bdat,
                                            u32 batch, u32 wid, u64* lds, u32 tid) {
     static_assert(NR == 2 || NR == 3, "k_block covers the last 8 (NR=2) or 12 (NR=3) stages");
     static_assert(SK == 0 || (SK == 3 && NR == 3), "k_block: SK = 3 needs NR = 3");
-    constexpr bool NTI = !(IM & 1), NTO = !(IM & 2);
+    constexpr int LDI = (IM & 4) ? LD_SC1 : ((IM & 1) ? LD_PLAIN : LD_NT);
+    constexpr bool NTO = !(IM & 2);
     const u32 logn = P.log_n;
     const u32 N = 1u << logn;
     const u32 G = N >> 12;  // blocks per polynomial
@@ -639,7 +647,7 @@ __device__ __forceinline__ void block_body(const PlanArgs& P, const u64* src, u6
         if (NR == 3) {
             // round 1: st = 256, p = tid + 256k
 #pragma unroll
-            for (int k = 0; k < 16; k++) v[k] = ld_m<NTI>(blk + tid + 256 * k);
+            for (int k = 0; k < 16; k++) v[k] = ld_m<LDI>(blk + tid + 256 * k);
             if (SK == 3)
                 fwd_stage16<3>(v, tw, (N >> 12) + g, M);  // input < 12q (k_tcols) -> < 12q
             else
@@ -652,7 +660,7 @@ __device__ __forceinline__ void block_body(const PlanArgs& P, const u64* src, u6
             for (int k = 0; k < 16; k++) v[k] = lds[L2 + 17 * k];
         } else {
 #pragma unroll
-            for (int k = 0; k < 16; k++) v[k] = ld_m<NTI>(blk + h * 256 + r + 16 * k);
+            for (int k = 0; k < 16; k++) v[k] = ld_m<LDI>(blk + h * 256 + r + 16 * k);
         }
         fwd_round16(v, tw, (N >> 8) + g * 16 + h, M);
 #pragma unroll
@@ -840,7 +848,8 @@ template <bool INV, bool SPQ, bool SWS = false, int LOGN = 16, int IM = 0>
 __device__ __forceinline__ void tcols_body(const PlanArgs& P, const u64* src, u64* dst, u32 batch, u32 wid,
                                            const SwSrc& SWA, u64* lds, u32 tid) {
     static_assert(LOGN == 16 || LOGN == 17, "k_tcols: N = 2^16 or 2^17");
-    constexpr bool NTI = !(IM & 1), NTO = !(IM & 2);
+    constexpr int LDI = (IM & 4) ? LD_SC1 : ((IM & 1) ? LD_PLAIN : LD_NT);
+    constexpr bool NTO = !(IM & 2);
     constexpr u32 N = 1u << LOGN, S = N / 256, W = TCOLS_W;
     // Exchange patterns p = tid + 16W k (round 1) and p = 16W h + W k + r
     // (round 2).  The inverse writes the second and reads the first: unpadded,
@@ -878,7 +887,7 @@ __device__ __forceinline__ void tcols_body(const PlanArgs& P, const u64* src, u6
             }
         } else {
 #pragma unroll
-            for (int k = 0; k < 16; k++) v[k] = ld_m<NTI>(x + (u64)(h + 16 * k) * S + r);
+            for (int k = 0; k < 16; k++) v[k] = ld_m<LDI>(x + (u64)(h + 16 * k) * S + r);
         }
         fwd_round16_canon(v, tw, 1, M);
 #pragma unroll
@@ -893,7 +902,7 @@ __device__ __forceinline__ void tcols_body(const PlanArgs& P, const u64* src, u6
     } else {
         const u64* itw = P.itw + (u64)t * N * 2;
 #pragma unroll
-        for (int k = 0; k < 16; k++) v[k] = ld_m<NTI>(x + (u64)(16 * h + k) * S + r);
+        for (int k = 0; k < 16; k++) v[k] = ld_m<LDI>(x + (u64)(16 * h + k) * S + r);
         if (OFHE_LAZY_GS) {
             // input < 4q (the block pass's lazy twist); round 2's registers all
             // come from one round-1 position, taken as < 8q

@@ -415,7 +415,7 @@ int ofhe_hip_plan_tune(ofhe_plan_t p, uint32_t chunk_batch, uint32_t streams) {
 static int pipe_probe(ofhe_plan_t p) {
     int occ = 0, ncu = 0;
     HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(
-        &occ, p->spq ? (const void*)k_pipe<true> : (const void*)k_pipe<false>, 256, 0));
+        &occ, p->spq ? (const void*)k_pipe<true, false> : (const void*)k_pipe<false, false>, 256, 0));
     HIPCHK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, p->ctx->device));
     if (occ < 1 || ncu < 1) return fail(OFHE_ERR_STATE, "persistent pipeline: kernel does not fit a CU");
     const u32 grid = (u32)occ * (u32)ncu;
@@ -459,12 +459,13 @@ int ofhe_hip_plan_pipeline(ofhe_plan_t p, int persistent, uint32_t lag) {
     if (p->pipe_state == 0) RCCHK(pipe_probe(p));
     if (p->pipe_state != 1) return fail(OFHE_ERR_STATE, "persistent pipeline: the XCD probe failed on this device");
     p->pipe_lag = lag ? lag : 4;
+    p->pipe_sc1 = getenv("OFHE_PIPE_SC1") && atoi(getenv("OFHE_PIPE_SC1")) != 0;  // A/B knob
     {
         // OFHE_PIPE_WGS: workgroups per CU (A/B knob: fewer in flight per XCD
         // means fewer towers' intermediates live in its L2); default: all fit
         int occ = 0, ncu = 0;
         HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(
-            &occ, p->spq ? (const void*)k_pipe<true> : (const void*)k_pipe<false>, 256, 0));
+            &occ, p->spq ? (const void*)k_pipe<true, false> : (const void*)k_pipe<false, false>, 256, 0));
         HIPCHK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, p->ctx->device));
         const char* w = getenv("OFHE_PIPE_WGS");
         if (w && atoi(w) > 0 && atoi(w) < occ) occ = atoi(w);
@@ -1093,10 +1094,13 @@ static int launch_pipe(ofhe_plan_t p, const PlanArgs& a, const u64* a_, const u6
     C.units = (u32)units;
     C.lag = p->pipe_lag;
     C.nq = p->pipe_nq;
-    if (p->spq)
-        hipLaunchKernelGGL(k_pipe<true>, dim3(p->pipe_grid), dim3(256), 0, s, a, a_, c, b, batch, C);
-    else
-        hipLaunchKernelGGL(k_pipe<false>, dim3(p->pipe_grid), dim3(256), 0, s, a, a_, c, b, batch, C);
+#define LP(SP, SC) hipLaunchKernelGGL((k_pipe<SP, SC>), dim3(p->pipe_grid), dim3(256), 0, s, a, a_, c, b, batch, C)
+    if (p->spq) {
+        if (p->pipe_sc1) LP(true, true); else LP(true, false);
+    } else {
+        if (p->pipe_sc1) LP(false, true); else LP(false, false);
+    }
+#undef LP
     HIPCHK(hipGetLastError());
     HIPCHK(hipFreeAsync(ctl, s));
     return post_launch();

@@ -59,7 +59,11 @@ struct PipeCtl {
     u32 nq;       // queues = XCDs
 };
 
-// workgroup-wide: wait until *ctr >= need, then acquire
+// workgroup-wide: wait until *ctr >= need, then (ACQ) acquire: the agent-scope
+// fence invalidates this CU's L1 asynchronously, and the s_waitcnt after it
+// holds the barrier until it has completed (MI355X_MICROARCH.md, "Consumer,
+// always"); without ACQ every load of the handed-off data must bypass L1 (sc1)
+template <bool ACQ>
 __device__ __forceinline__ void pipe_wait(u32* ctr, u32 need, u32* err) {
     if (threadIdx.x == 0) {
         u32 spins = 0;
@@ -74,7 +78,10 @@ __device__ __forceinline__ void pipe_wait(u32* ctr, u32 need, u32* err) {
                 break;
             }
         }
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        if (ACQ) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
     }
     __syncthreads();
 }
@@ -86,7 +93,9 @@ __device__ __forceinline__ void pipe_signal(u32* ctr) {
     if (threadIdx.x == 0) __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-template <bool SPQ>
+// SC1: the B and I phases load their inputs with sc1 (L1 bypass) instead of
+// invalidating L1 with an acquire per item (A/B: OFHE_PIPE_SC1)
+template <bool SPQ, bool SC1>
 __global__ __launch_bounds__(256, OFHE_KB_WAVES) void k_pipe(PlanArgs P, const u64* a, u64* c,
                                                              const u64* __restrict__ b, u32 batch, PipeCtl C) {
     OFHE_VGPR_FLOOR();
@@ -121,12 +130,12 @@ __global__ __launch_bounds__(256, OFHE_KB_WAVES) void k_pipe(PlanArgs P, const u
                 tcols_body<false, SPQ, false, 16, 2>(P, a, c, batch, wid, none, lds, ti);
                 pipe_signal(C.done_f + u);
             } else if (ph == 1) {
-                pipe_wait(C.done_f + u, PIPE_PIECES, C.err);
-                block_body<MODE_FUSED, SPQ, 2, 0, 3>(P, c, c, b, batch, wid, lds, ti);
+                pipe_wait<!SC1>(C.done_f + u, PIPE_PIECES, C.err);
+                block_body<MODE_FUSED, SPQ, 2, 0, SC1 ? 7 : 3>(P, c, c, b, batch, wid, lds, ti);
                 pipe_signal(C.done_b + u);
             } else {
-                pipe_wait(C.done_b + u, PIPE_PIECES, C.err);
-                tcols_body<true, SPQ, false, 16, 1>(P, c, c, batch, wid, none, lds, ti);
+                pipe_wait<!SC1>(C.done_b + u, PIPE_PIECES, C.err);
+                tcols_body<true, SPQ, false, 16, SC1 ? 5 : 1>(P, c, c, batch, wid, none, lds, ti);
             }
         }
         __syncthreads();  // LDS and s_next free
