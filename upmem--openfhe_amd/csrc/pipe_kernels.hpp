@@ -95,6 +95,14 @@ __device__ __forceinline__ void pipe_signal(u32* ctr) {
 
 // SC1: the B and I phases load their inputs with sc1 (L1 bypass) instead of
 // invalidating L1 with an acquire per item (A/B: OFHE_PIPE_SC1)
+#ifndef OFHE_PIPE_EARLY_CLAIM
+#define OFHE_PIPE_EARLY_CLAIM 0
+#endif
+__device__ __forceinline__ void pipe_claim(u32* head, u32& nxt) {
+    if (!OFHE_PIPE_EARLY_CLAIM && threadIdx.x == 0)
+        nxt = __hip_atomic_fetch_add(head, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 template <bool SPQ, bool SC1>
 __global__ __launch_bounds__(256, OFHE_KB_WAVES) void k_pipe(PlanArgs P, const u64* a, u64* c,
                                                              const u64* __restrict__ b, u32 batch, PipeCtl C) {
@@ -111,9 +119,14 @@ __global__ __launch_bounds__(256, OFHE_KB_WAVES) void k_pipe(PlanArgs P, const u
     __syncthreads();
     u32 item = __builtin_amdgcn_readfirstlane(s_next);  // wave-uniform: kept in SGPRs
     while (item < total) {
-        // claim the next item now; its latency hides under this one
+        // the next item is claimed when this one's loads are all consumed (its
+        // last stores are in flight): a returning atomic issued earlier would
+        // hold every load wait of the claiming wave behind its round trip
+        // (vmcnt counts in order), OFHE_PIPE_EARLY_CLAIM = 1 claims at the top
         u32 nxt = 0;
+#if OFHE_PIPE_EARLY_CLAIM
         if (tid == 0) nxt = __hip_atomic_fetch_add(head, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#endif
         const u32 step = item / PIPE_STEP, slot = item % PIPE_STEP;
         const u32 ph = slot / PIPE_PIECES, piece = slot % PIPE_PIECES;
         if (step >= ph * C.lag && step - ph * C.lag < nu) {
@@ -128,15 +141,20 @@ __global__ __launch_bounds__(256, OFHE_KB_WAVES) void k_pipe(PlanArgs P, const u
             asm volatile("" : "+v"(ti));
             if (ph == 0) {
                 tcols_body<false, SPQ, false, 16, 2>(P, a, c, batch, wid, none, lds, ti);
+                pipe_claim(head, nxt);
                 pipe_signal(C.done_f + u);
             } else if (ph == 1) {
                 pipe_wait<!SC1>(C.done_f + u, PIPE_PIECES, C.err);
                 block_body<MODE_FUSED, SPQ, 2, 0, SC1 ? 7 : 3>(P, c, c, b, batch, wid, lds, ti);
+                pipe_claim(head, nxt);
                 pipe_signal(C.done_b + u);
             } else {
                 pipe_wait<!SC1>(C.done_b + u, PIPE_PIECES, C.err);
                 tcols_body<true, SPQ, false, 16, SC1 ? 5 : 1>(P, c, c, batch, wid, none, lds, ti);
+                pipe_claim(head, nxt);
             }
+        } else {
+            pipe_claim(head, nxt);
         }
         __syncthreads();  // LDS and s_next free
         if (tid == 0) s_next = nxt;
