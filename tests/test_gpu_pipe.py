@@ -13,14 +13,31 @@ from test_gpu_parity import dev, host, stream
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("sc1", [False, True])
+# knob settings read by ofhe_hip_plan_pipeline: hand-off by acquire + plain
+# loads or by sc1 loads; dynamic queue or static item assignment; pieces per item
+CFGS = {
+    "acq": {"OFHE_PIPE_SC1": "0"},
+    "sc1": {"OFHE_PIPE_SC1": "1"},
+    "static_p4": {"OFHE_PIPE_SC1": "1", "OFHE_PIPE_STATIC": "1", "OFHE_PIPE_PIECES": "4"},
+    "dyn_p2_acq": {"OFHE_PIPE_SC1": "0", "OFHE_PIPE_PIECES": "2"},
+}
+
+
+def _cfg(monkeypatch, name):
+    for k in ("OFHE_PIPE_SC1", "OFHE_PIPE_STATIC", "OFHE_PIPE_PIECES"):
+        monkeypatch.delenv(k, raising=False)
+    for k, v in CFGS[name].items():
+        monkeypatch.setenv(k, v)
+
+
+@pytest.mark.parametrize("cfg", sorted(CFGS))
 @pytest.mark.parametrize("T,B", [(1, 1), (1, 5), (3, 7), (16, 2), (5, 13)])
-def test_pipe_vs_oracle(hip, T, B, sc1, monkeypatch):
-    """Both hand-off forms: acquire + plain loads, and sc1 loads (OFHE_PIPE_SC1)."""
+def test_pipe_vs_oracle(hip, T, B, cfg, monkeypatch):
+    """Every knob setting of the persistent pipeline against the oracle."""
     import torch
 
     H, ctx = hip
-    monkeypatch.setenv("OFHE_PIPE_SC1", "1" if sc1 else "0")
+    _cfg(monkeypatch, cfg)
     log_n = 16
     n = 1 << log_n
     qs, rs = O.moduli_chain(log_n, T)
@@ -73,15 +90,15 @@ def test_pipe_edge_values_generic_moduli(hip, monkeypatch):
     plan.close()
 
 
-@pytest.mark.parametrize("sc1", [False, True])
-def test_pipe_full_batch_matches_three_launches(hip, sc1, monkeypatch):
+@pytest.mark.parametrize("cfg", sorted(CFGS))
+def test_pipe_full_batch_matches_three_launches(hip, cfg, monkeypatch):
     """configs[2] (N = 2^16, 16 towers, batch 1024, 8 GiB per operand): the
     persistent pipeline's c equals the three-launch pipeline's, every word, and
     sampled rows equal the oracle."""
     import torch
 
     H, ctx = hip
-    monkeypatch.setenv("OFHE_PIPE_SC1", "1" if sc1 else "0")
+    _cfg(monkeypatch, cfg)
     log_n, T, B = 16, 16, 1024
     n = 1 << log_n
     qs, rs = O.moduli_chain(log_n, T)

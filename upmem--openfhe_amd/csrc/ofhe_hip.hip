@@ -459,7 +459,14 @@ int ofhe_hip_plan_pipeline(ofhe_plan_t p, int persistent, uint32_t lag) {
     if (p->pipe_state == 0) RCCHK(pipe_probe(p));
     if (p->pipe_state != 1) return fail(OFHE_ERR_STATE, "persistent pipeline: the XCD probe failed on this device");
     p->pipe_lag = lag ? lag : 4;
-    p->pipe_sc1 = getenv("OFHE_PIPE_SC1") && atoi(getenv("OFHE_PIPE_SC1")) != 0;  // A/B knob
+    // A/B knobs: sc1 hand-off loads, pieces per work item, static item assignment
+    p->pipe_sc1 = getenv("OFHE_PIPE_SC1") && atoi(getenv("OFHE_PIPE_SC1")) != 0;
+    {
+        const char* e = getenv("OFHE_PIPE_PIECES");
+        const u32 v = e ? (u32)atoi(e) : 1;
+        p->pipe_pieces = (v == 2 || v == 4 || v == 8 || v == 16) ? v : 1;
+        p->pipe_static = getenv("OFHE_PIPE_STATIC") && atoi(getenv("OFHE_PIPE_STATIC")) != 0;
+    }
     {
         // OFHE_PIPE_WGS: workgroups per CU (A/B knob: fewer in flight per XCD
         // means fewer towers' intermediates live in its L2); default: all fit
@@ -1079,7 +1086,7 @@ static int launch_pipe(ofhe_plan_t p, const PlanArgs& a, const u64* a_, const u6
                        hipStream_t s) {
     const u64 units = (u64)batch * p->towers;
     if (units * PIPE_PIECES >= (1ull << 32)) return fail(OFHE_ERR_ARG, "batch too large for the persistent pipeline");
-    const size_t words = (size_t)(p->pipe_nq + 1) * PIPE_QSTRIDE + 2 * units;
+    const size_t words = (size_t)(2 * p->pipe_nq + 1) * PIPE_QSTRIDE + 2 * units;
     void* ctl = nullptr;
     hipError_t e = p->ctx->pool ? hipMallocFromPoolAsync(&ctl, words * 4, p->ctx->pool, s)
                                 : hipMallocAsync(&ctl, words * 4, s);
@@ -1087,13 +1094,16 @@ static int launch_pipe(ofhe_plan_t p, const PlanArgs& a, const u64* a_, const u6
     HIPCHK(hipMemsetAsync(ctl, 0, words * 4, s));
     PipeCtl C;
     C.head = (u32*)ctl;
-    C.exited = C.head + (size_t)p->pipe_nq * PIPE_QSTRIDE;
+    C.members = C.head + (size_t)p->pipe_nq * PIPE_QSTRIDE;
+    C.exited = C.members + (size_t)p->pipe_nq * PIPE_QSTRIDE;
     C.done_f = C.exited + PIPE_QSTRIDE;
     C.done_b = C.done_f + units;
     C.err = p->d_pipe_err;
     C.units = (u32)units;
     C.lag = p->pipe_lag;
     C.nq = p->pipe_nq;
+    C.pieces = p->pipe_pieces;
+    C.wpq = p->pipe_static ? p->pipe_grid / p->pipe_nq : 0;
 #define LP(SP, SC) hipLaunchKernelGGL((k_pipe<SP, SC>), dim3(p->pipe_grid), dim3(256), 0, s, a, a_, c, b, batch, C)
     if (p->spq) {
         if (p->pipe_sc1) LP(true, true); else LP(true, false);

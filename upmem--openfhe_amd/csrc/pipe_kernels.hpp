@@ -53,10 +53,13 @@ struct PipeCtl {
     u32* done_f;  // [units] forward column tiles finished
     u32* done_b;  // [units] block-pass blocks finished
     u32* exited;  // [1] workgroups that have left the item loop
+    u32* members; // [nq * PIPE_QSTRIDE] static mode: workgroups that joined each queue
     u32* err;     // [1] per plan: waits that gave up + queues left undrained (never expected)
     u32 units;    // batch * towers
     u32 lag;      // steps between a unit's phases (>= 1)
     u32 nq;       // queues = XCDs
+    u32 pieces;   // pieces (tiles / blocks) per work item: 1, 2, 4, 8 or 16
+    u32 wpq;      // 0: dynamic queue; else static, workgroups per queue
 };
 
 // workgroup-wide: wait until *ctr >= need, then (ACQ) acquire: the agent-scope
@@ -86,11 +89,12 @@ __device__ __forceinline__ void pipe_wait(u32* ctr, u32 need, u32* err) {
     __syncthreads();
 }
 
-// workgroup-wide: every thread's stores have reached L2, then count the item
-__device__ __forceinline__ void pipe_signal(u32* ctr) {
+// workgroup-wide: every thread's stores have reached L2, then count the item's
+// pieces
+__device__ __forceinline__ void pipe_signal(u32* ctr, u32 pieces) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (threadIdx.x == 0) __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (threadIdx.x == 0) __hip_atomic_fetch_add(ctr, pieces, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // SC1: the B and I phases load their inputs with sc1 (L1 bypass) instead of
@@ -112,63 +116,77 @@ __global__ __launch_bounds__(256, OFHE_KB_WAVES) void k_pipe(PlanArgs P, const u
     const u32 tid = threadIdx.x;
     const u32 q = xcc_id() % C.nq;
     const u32 nu = C.units > q ? (C.units - q + C.nq - 1) / C.nq : 0;  // units of this queue
-    const u32 total = nu ? (nu + 2 * C.lag) * PIPE_STEP : 0;
+    const u32 ipp = PIPE_PIECES / C.pieces;  // items per phase of a unit
+    const u32 total = nu ? (nu + 2 * C.lag) * 3 * ipp : 0;
     u32* head = C.head + PIPE_QSTRIDE * q;
     const SwSrc none{nullptr, 0, 0, nullptr, 1, 0};
-    if (tid == 0) s_next = __hip_atomic_fetch_add(head, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // dynamic (C.wpq = 0): items from the queue head; static: the r-th
+    // workgroup of this XCD takes items r, r + wpq, r + 2 wpq, ... (no claim
+    // per item; deadlock-free too: the lowest unfinished item never waits)
+    if (tid == 0) s_next = __hip_atomic_fetch_add(C.wpq ? C.members + PIPE_QSTRIDE * q : head, 1u, __ATOMIC_RELAXED,
+                                                  __HIP_MEMORY_SCOPE_AGENT);
     __syncthreads();
     u32 item = __builtin_amdgcn_readfirstlane(s_next);  // wave-uniform: kept in SGPRs
+    if (C.wpq && item >= C.wpq) item = total;             // more workgroups on this XCD than planned
     while (item < total) {
         // the next item is claimed when this one's loads are all consumed (its
         // last stores are in flight): a returning atomic issued earlier would
         // hold every load wait of the claiming wave behind its round trip
         // (vmcnt counts in order), OFHE_PIPE_EARLY_CLAIM = 1 claims at the top
-        u32 nxt = 0;
+        u32 nxt = item + C.wpq;
 #if OFHE_PIPE_EARLY_CLAIM
-        if (tid == 0) nxt = __hip_atomic_fetch_add(head, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (!C.wpq && tid == 0) nxt = __hip_atomic_fetch_add(head, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #endif
-        const u32 step = item / PIPE_STEP, slot = item % PIPE_STEP;
-        const u32 ph = slot / PIPE_PIECES, piece = slot % PIPE_PIECES;
+        const u32 step = item / (3 * ipp), slot = item % (3 * ipp);
+        const u32 ph = slot / ipp, grp = slot % ipp;
         if (step >= ph * C.lag && step - ph * C.lag < nu) {
             const u32 u = q + C.nq * (step - ph * C.lag);
-            const u32 wid = u * PIPE_PIECES + piece;
-            // a fresh copy of the thread index per item: without it LLVM hoists
-            // every phase's thread-index arithmetic (LDS and global offsets) out
-            // of the loop, all of it stays live across all three phases, and
-            // the kernel spills (312 B of scratch at 128 VGPRs; 116 VGPRs and
-            // no scratch with this)
-            u32 ti = tid;
-            asm volatile("" : "+v"(ti));
-            if (ph == 0) {
-                tcols_body<false, SPQ, false, 16, 2>(P, a, c, batch, wid, none, lds, ti);
-                pipe_claim(head, nxt);
-                pipe_signal(C.done_f + u);
-            } else if (ph == 1) {
-                pipe_wait<!SC1>(C.done_f + u, PIPE_PIECES, C.err);
-                block_body<MODE_FUSED, SPQ, 2, 0, SC1 ? 7 : 3>(P, c, c, b, batch, wid, lds, ti);
-                pipe_claim(head, nxt);
-                pipe_signal(C.done_b + u);
-            } else {
-                pipe_wait<!SC1>(C.done_b + u, PIPE_PIECES, C.err);
-                tcols_body<true, SPQ, false, 16, SC1 ? 5 : 1>(P, c, c, batch, wid, none, lds, ti);
-                pipe_claim(head, nxt);
+            if (ph == 1) pipe_wait<!SC1>(C.done_f + u, PIPE_PIECES, C.err);
+            if (ph == 2) pipe_wait<!SC1>(C.done_b + u, PIPE_PIECES, C.err);
+            for (u32 k = 0; k < C.pieces; k++) {
+                const u32 wid = u * PIPE_PIECES + grp * C.pieces + k;
+                // a fresh copy of the thread index per piece: without it LLVM
+                // hoists every phase's thread-index arithmetic (LDS and global
+                // offsets) out of the loop, all of it stays live across all
+                // three phases, and the kernel spills (312 B of scratch at 128
+                // VGPRs; 116 VGPRs and no scratch with this)
+                u32 ti = tid;
+                asm volatile("" : "+v"(ti));
+                if (k) __syncthreads();  // the previous piece's LDS reads are done
+                if (ph == 0)
+                    tcols_body<false, SPQ, false, 16, 2>(P, a, c, batch, wid, none, lds, ti);
+                else if (ph == 1)
+                    block_body<MODE_FUSED, SPQ, 2, 0, SC1 ? 7 : 3>(P, c, c, b, batch, wid, lds, ti);
+                else
+                    tcols_body<true, SPQ, false, 16, SC1 ? 5 : 1>(P, c, c, batch, wid, none, lds, ti);
             }
-        } else {
+            if (!C.wpq) pipe_claim(head, nxt);
+            if (ph == 0) pipe_signal(C.done_f + u, C.pieces);
+            if (ph == 1) pipe_signal(C.done_b + u, C.pieces);
+        } else if (!C.wpq) {
             pipe_claim(head, nxt);
         }
-        __syncthreads();  // LDS and s_next free
-        if (tid == 0) s_next = nxt;
-        __syncthreads();
-        item = __builtin_amdgcn_readfirstlane(s_next);
+        if (C.wpq) {
+            item = nxt;
+            __syncthreads();  // LDS free
+        } else {
+            __syncthreads();  // LDS and s_next free
+            if (tid == 0) s_next = nxt;
+            __syncthreads();
+            item = __builtin_amdgcn_readfirstlane(s_next);
+        }
     }
     // audit by the last workgroup out: every queue with units was drained
-    // (a queue no workgroup ran on would leave its towers unwritten)
+    // (dynamic) or had all its planned workgroups (static); a queue no
+    // workgroup ran on would leave its towers unwritten
     if (tid == 0 && __hip_atomic_fetch_add(C.exited, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1) {
         for (u32 x = 0; x < C.nq; x++) {
             const u32 n = C.units > x ? (C.units - x + C.nq - 1) / C.nq : 0;
-            if (n && __hip_atomic_load(C.head + PIPE_QSTRIDE * x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <
-                         (n + 2 * C.lag) * PIPE_STEP)
-                __hip_atomic_fetch_add(C.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const bool bad =
+                C.wpq ? __hip_atomic_load(C.members + PIPE_QSTRIDE * x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < C.wpq
+                      : __hip_atomic_load(C.head + PIPE_QSTRIDE * x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <
+                            (n + 2 * C.lag) * 3 * ipp;
+            if (n && bad) __hip_atomic_fetch_add(C.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
 }
