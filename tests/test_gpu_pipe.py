@@ -16,15 +16,15 @@ pytestmark = pytest.mark.gpu
 # knob settings read by ofhe_hip_plan_pipeline: hand-off by acquire + plain
 # loads or by sc1 loads; dynamic queue or static item assignment; pieces per item
 CFGS = {
-    "acq": {"OFHE_PIPE_SC1": "0"},
-    "sc1": {"OFHE_PIPE_SC1": "1"},
-    "static_p4": {"OFHE_PIPE_SC1": "1", "OFHE_PIPE_STATIC": "1", "OFHE_PIPE_PIECES": "4"},
-    "dyn_p2_acq": {"OFHE_PIPE_SC1": "0", "OFHE_PIPE_PIECES": "2"},
+    "acq": {"OFHE_PIPE_HM": "0"},
+    "sc1": {"OFHE_PIPE_HM": "1"},
+    "static_p4_nt": {"OFHE_PIPE_HM": "2", "OFHE_PIPE_STATIC": "1", "OFHE_PIPE_PIECES": "4"},
+    "dyn_p2_acq_nt": {"OFHE_PIPE_HM": "3", "OFHE_PIPE_PIECES": "2"},
 }
 
 
 def _cfg(monkeypatch, name):
-    for k in ("OFHE_PIPE_SC1", "OFHE_PIPE_STATIC", "OFHE_PIPE_PIECES"):
+    for k in ("OFHE_PIPE_HM", "OFHE_PIPE_STATIC", "OFHE_PIPE_PIECES"):
         monkeypatch.delenv(k, raising=False)
     for k, v in CFGS[name].items():
         monkeypatch.setenv(k, v)

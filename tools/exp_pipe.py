@@ -2,7 +2,7 @@
 against the persistent one-launch k_pipe (ofhe_hip_plan_pipeline) at several
 lags, interleaved rounds, HIP events on the launch stream; every variant's c
 must equal the three-launch c.
-  EXP_BATCH (1024), EXP_ROUNDS (6), EXP_LAGS ("12s,8p2s,8p4s,12p2ts,8p4ts,12p4ts,16p4ts": lag, optionally w<workgroups per CU>)"""
+  EXP_BATCH (1024), EXP_ROUNDS (6), EXP_LAGS ("12h0,12h1,12h2,12h3,6h2,8h2,16h2,12p2h2": lag, optionally w<workgroups per CU>)"""
 import os
 import re
 import statistics
@@ -31,20 +31,20 @@ plan.fill_uniform(b.data_ptr(), B, 2, 0, sp)
 plan.ntt_mul_intt(a.data_ptr(), b.data_ptr(), c.data_ptr(), B, sp)
 ref = c.clone()
 # variants: "three", or "pipe<lag>[w<workgroups per CU>][p<pieces per item>][t][s]"
-# (t: static item assignment, s: sc1 hand-off loads)
-variants = ["three"] + ["pipe" + x for x in os.environ.get("EXP_LAGS", "12s,8p2s,8p4s,12p2ts,8p4ts,12p4ts,16p4ts").split(",")]
+# (t: static item assignment, h: k_pipe hand-off mode HM)
+variants = ["three"] + ["pipe" + x for x in os.environ.get("EXP_LAGS", "12h0,12h1,12h2,12h3,6h2,8h2,16h2,12p2h2").split(",")]
 times = {v: [] for v in variants}
 for rnd in range(int(os.environ.get("EXP_ROUNDS", "6"))):
     for v in (variants if rnd % 2 == 0 else variants[::-1]):
         if v == "three":
             plan.pipeline(False)
         else:
-            m = re.fullmatch(r"(\d+)(?:w(\d+))?(?:p(\d+))?(t?)(s?)", v[4:])
-            lag, w, pcs, st, sc = m.groups()
+            m = re.fullmatch(r"(\d+)(?:w(\d+))?(?:p(\d+))?(t?)(?:h(\d))?", v[4:])
+            lag, w, pcs, st, hm = m.groups()
             os.environ["OFHE_PIPE_WGS"] = w or ""
             os.environ["OFHE_PIPE_PIECES"] = pcs or "1"
             os.environ["OFHE_PIPE_STATIC"] = "1" if st else "0"
-            os.environ["OFHE_PIPE_SC1"] = "1" if sc else "0"
+            os.environ["OFHE_PIPE_HM"] = hm or "1"
             plan.pipeline(True, int(lag))
         c.zero_()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)

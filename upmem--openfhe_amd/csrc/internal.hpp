@@ -152,8 +152,8 @@ struct ofhe_plan_s {
     // persistent pipeline (k_pipe, pipe_kernels.hpp; ofhe_hip_plan_pipeline):
     // selected, lag, grid, and the one-time XCD probe (0 not run, 1 passed,
     // -1 failed / not applicable); d_pipe_err counts given-up waits
-    bool pipe = false, pipe_sc1 = false, pipe_static = false;
-    ofhe::u32 pipe_lag = 4, pipe_grid = 0, pipe_nq = 8, pipe_pieces = 1;
+    bool pipe = false, pipe_static = false;
+    ofhe::u32 pipe_lag = 4, pipe_grid = 0, pipe_nq = 8, pipe_pieces = 1, pipe_hm = 1;
     int pipe_state = 0;
     ofhe::u32* d_pipe_err = nullptr;
     bool spq = false;     // every modulus is 2^L - d with d < 2^32 (special-prime kernels)

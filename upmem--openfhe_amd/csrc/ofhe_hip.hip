@@ -415,7 +415,7 @@ int ofhe_hip_plan_tune(ofhe_plan_t p, uint32_t chunk_batch, uint32_t streams) {
 static int pipe_probe(ofhe_plan_t p) {
     int occ = 0, ncu = 0;
     HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(
-        &occ, p->spq ? (const void*)k_pipe<true, false> : (const void*)k_pipe<false, false>, 256, 0));
+        &occ, p->spq ? (const void*)k_pipe<true, 1> : (const void*)k_pipe<false, 1>, 256, 0));
     HIPCHK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, p->ctx->device));
     if (occ < 1 || ncu < 1) return fail(OFHE_ERR_STATE, "persistent pipeline: kernel does not fit a CU");
     const u32 grid = (u32)occ * (u32)ncu;
@@ -459,8 +459,8 @@ int ofhe_hip_plan_pipeline(ofhe_plan_t p, int persistent, uint32_t lag) {
     if (p->pipe_state == 0) RCCHK(pipe_probe(p));
     if (p->pipe_state != 1) return fail(OFHE_ERR_STATE, "persistent pipeline: the XCD probe failed on this device");
     p->pipe_lag = lag ? lag : 4;
-    // A/B knobs: sc1 hand-off loads, pieces per work item, static item assignment
-    p->pipe_sc1 = getenv("OFHE_PIPE_SC1") && atoi(getenv("OFHE_PIPE_SC1")) != 0;
+    // A/B knobs: hand-off mode (k_pipe HM), pieces per work item, static item assignment
+    p->pipe_hm = getenv("OFHE_PIPE_HM") ? (u32)atoi(getenv("OFHE_PIPE_HM")) & 3 : 1;
     {
         const char* e = getenv("OFHE_PIPE_PIECES");
         const u32 v = e ? (u32)atoi(e) : 1;
@@ -472,7 +472,7 @@ int ofhe_hip_plan_pipeline(ofhe_plan_t p, int persistent, uint32_t lag) {
         // means fewer towers' intermediates live in its L2); default: all fit
         int occ = 0, ncu = 0;
         HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(
-            &occ, p->spq ? (const void*)k_pipe<true, false> : (const void*)k_pipe<false, false>, 256, 0));
+            &occ, p->spq ? (const void*)k_pipe<true, 1> : (const void*)k_pipe<false, 1>, 256, 0));
         HIPCHK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, p->ctx->device));
         const char* w = getenv("OFHE_PIPE_WGS");
         if (w && atoi(w) > 0 && atoi(w) < occ) occ = atoi(w);
@@ -1104,11 +1104,16 @@ static int launch_pipe(ofhe_plan_t p, const PlanArgs& a, const u64* a_, const u6
     C.nq = p->pipe_nq;
     C.pieces = p->pipe_pieces;
     C.wpq = p->pipe_static ? p->pipe_grid / p->pipe_nq : 0;
-#define LP(SP, SC) hipLaunchKernelGGL((k_pipe<SP, SC>), dim3(p->pipe_grid), dim3(256), 0, s, a, a_, c, b, batch, C)
-    if (p->spq) {
-        if (p->pipe_sc1) LP(true, true); else LP(true, false);
+#define LP(SP, HM) hipLaunchKernelGGL((k_pipe<SP, HM>), dim3(p->pipe_grid), dim3(256), 0, s, a, a_, c, b, batch, C)
+    if (!p->spq) {
+        LP(false, 1);  // generic moduli: one hand-off form
     } else {
-        if (p->pipe_sc1) LP(false, true); else LP(false, false);
+        switch (p->pipe_hm) {
+            case 0: LP(true, 0); break;
+            case 2: LP(true, 2); break;
+            case 3: LP(true, 3); break;
+            default: LP(true, 1); break;
+        }
     }
 #undef LP
     HIPCHK(hipGetLastError());

@@ -97,8 +97,6 @@ __device__ __forceinline__ void pipe_signal(u32* ctr, u32 pieces) {
     if (threadIdx.x == 0) __hip_atomic_fetch_add(ctr, pieces, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// SC1: the B and I phases load their inputs with sc1 (L1 bypass) instead of
-// invalidating L1 with an acquire per item (A/B: OFHE_PIPE_SC1)
 #ifndef OFHE_PIPE_EARLY_CLAIM
 #define OFHE_PIPE_EARLY_CLAIM 0
 #endif
@@ -107,7 +105,10 @@ __device__ __forceinline__ void pipe_claim(u32* head, u32& nxt) {
         nxt = __hip_atomic_fetch_add(head, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-template <bool SPQ, bool SC1>
+// HM, the hand-off mode of the intermediates: 0 acquire + plain loads, plain
+// stores; 1 sc1 loads (no acquire), plain stores; 2 sc1 loads, non-temporal
+// stores; 3 acquire + non-temporal loads and stores
+template <bool SPQ, int HM>
 __global__ __launch_bounds__(256, OFHE_KB_WAVES) void k_pipe(PlanArgs P, const u64* a, u64* c,
                                                              const u64* __restrict__ b, u32 batch, PipeCtl C) {
     OFHE_VGPR_FLOOR();
@@ -120,6 +121,9 @@ __global__ __launch_bounds__(256, OFHE_KB_WAVES) void k_pipe(PlanArgs P, const u
     const u32 total = nu ? (nu + 2 * C.lag) * 3 * ipp : 0;
     u32* head = C.head + PIPE_QSTRIDE * q;
     const SwSrc none{nullptr, 0, 0, nullptr, 1, 0};
+    constexpr bool SC1 = HM == 1 || HM == 2;
+    constexpr int OUT = (HM >= 2) ? 0 : 2;                  // IM bit 1: cached intermediate stores
+    constexpr int IN = SC1 ? 4 : (HM == 3 ? 0 : 1);         // IM bits 0 / 2: plain or sc1 intermediate loads
     // dynamic (C.wpq = 0): items from the queue head; static: the r-th
     // workgroup of this XCD takes items r, r + wpq, r + 2 wpq, ... (no claim
     // per item; deadlock-free too: the lowest unfinished item never waits)
@@ -154,11 +158,11 @@ __global__ __launch_bounds__(256, OFHE_KB_WAVES) void k_pipe(PlanArgs P, const u
                 asm volatile("" : "+v"(ti));
                 if (k) __syncthreads();  // the previous piece's LDS reads are done
                 if (ph == 0)
-                    tcols_body<false, SPQ, false, 16, 2>(P, a, c, batch, wid, none, lds, ti);
+                    tcols_body<false, SPQ, false, 16, OUT>(P, a, c, batch, wid, none, lds, ti);
                 else if (ph == 1)
-                    block_body<MODE_FUSED, SPQ, 2, 0, SC1 ? 7 : 3>(P, c, c, b, batch, wid, lds, ti);
+                    block_body<MODE_FUSED, SPQ, 2, 0, IN | OUT>(P, c, c, b, batch, wid, lds, ti);
                 else
-                    tcols_body<true, SPQ, false, 16, SC1 ? 5 : 1>(P, c, c, batch, wid, none, lds, ti);
+                    tcols_body<true, SPQ, false, 16, IN>(P, c, c, batch, wid, none, lds, ti);
             }
             if (!C.wpq) pipe_claim(head, nxt);
             if (ph == 0) pipe_signal(C.done_f + u, C.pieces);
