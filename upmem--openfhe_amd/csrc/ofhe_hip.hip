@@ -447,7 +447,7 @@ static int pipe_probe(ofhe_plan_t p) {
 
 int ofhe_hip_plan_pipeline(ofhe_plan_t p, int persistent, uint32_t lag) {
     if (!p || !p->ctx) return fail(OFHE_ERR_STATE, "plan is NULL or destroyed");
-    if (lag > 256) return fail(OFHE_ERR_ARG, "lag must be <= 256");
+    if (lag > (1u << 20)) return fail(OFHE_ERR_ARG, "lag must be <= 2^20");
     HIPCHK(hipSetDevice(p->ctx->device));
     std::lock_guard<std::mutex> lk(p->fork_mu);
     if (!persistent) {
