@@ -137,18 +137,20 @@ __global__ __launch_bounds__(256, OFHE_KB_WAVES) void k_pipe(PlanArgs P, const u
         // last stores are in flight): a returning atomic issued earlier would
         // hold every load wait of the claiming wave behind its round trip
         // (vmcnt counts in order), OFHE_PIPE_EARLY_CLAIM = 1 claims at the top
-        u32 nxt = item + C.wpq;
+        u32 nxt = 0;
 #if OFHE_PIPE_EARLY_CLAIM
         if (!C.wpq && tid == 0) nxt = __hip_atomic_fetch_add(head, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #endif
         const u32 step = item / (3 * ipp), slot = item % (3 * ipp);
         const u32 ph = slot / ipp, grp = slot % ipp;
         if (step >= ph * C.lag && step - ph * C.lag < nu) {
-            const u32 u = q + C.nq * (step - ph * C.lag);
+            // every index below is wave-uniform; readfirstlane tells LLVM so,
+            // which keeps the tower constants and table bases in scalar loads
+            const u32 u = __builtin_amdgcn_readfirstlane(q + C.nq * (step - ph * C.lag));
             if (ph == 1) pipe_wait<!SC1>(C.done_f + u, PIPE_PIECES, C.err);
             if (ph == 2) pipe_wait<!SC1>(C.done_b + u, PIPE_PIECES, C.err);
             for (u32 k = 0; k < C.pieces; k++) {
-                const u32 wid = u * PIPE_PIECES + grp * C.pieces + k;
+                const u32 wid = __builtin_amdgcn_readfirstlane(u * PIPE_PIECES + grp * C.pieces + k);
                 // a fresh copy of the thread index per piece: without it LLVM
                 // hoists every phase's thread-index arithmetic (LDS and global
                 // offsets) out of the loop, all of it stays live across all
@@ -171,7 +173,7 @@ __global__ __launch_bounds__(256, OFHE_KB_WAVES) void k_pipe(PlanArgs P, const u
             pipe_claim(head, nxt);
         }
         if (C.wpq) {
-            item = nxt;
+            item = __builtin_amdgcn_readfirstlane(item + C.wpq);  // uniform (nxt may hold a lane-0 claim)
             __syncthreads();  // LDS free
         } else {
             __syncthreads();  // LDS and s_next free
