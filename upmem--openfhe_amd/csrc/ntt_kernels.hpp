@@ -841,6 +841,9 @@ static_assert(TCOLS_W == 16 || TCOLS_W == 32, "column tile width");
 // same 256-row sub-transforms on 512 columns (the twiddle index of stage m is
 // m + row / (256 / m) whatever the row length).
 constexpr u32 TCOLS_LDS_WORDS = 16 * 16 * TCOLS_W + 16 * 16;
+#ifndef OFHE_TCOLS_LOOP
+#define OFHE_TCOLS_LOOP 1  // tiles per workgroup (diagnostic variant builds only)
+#endif
 // The body of k_tcols for work item wid (column tile cb = wid % (S / W) of
 // polynomial tower pb = wid / (S / W)) on the caller's LDS (TCOLS_LDS_WORDS);
 // IM as block_body's.
@@ -941,7 +944,20 @@ __global__ __launch_bounds__(16 * TCOLS_W, OFHE_KB_WAVES) void k_tcols(PlanArgs 
                                                                        u32 batch, u32 nwg, SwSrc SWA) {
     OFHE_VGPR_FLOOR();
     __shared__ u64 lds[TCOLS_LDS_WORDS];
+#if OFHE_TCOLS_LOOP > 1
+    // diagnostic (persistent-loop cost): each workgroup runs OFHE_TCOLS_LOOP
+    // tiles back to back, the grid shrunk by that factor (N = 2^16 launches)
+    for (u32 k = 0; k < OFHE_TCOLS_LOOP; k++) {
+        u32 ti = threadIdx.x;
+        asm volatile("" : "+v"(ti));
+        const u32 it = blockIdx.x + k * gridDim.x;
+        if (it >= nwg) break;  // launch sites that still size the grid to nwg
+        if (k) __syncthreads();
+        tcols_body<INV, SPQ, SWS, LOGN>(P, src, dst, batch, xcd_remap(it, nwg), SWA, lds, ti);
+    }
+#else
     tcols_body<INV, SPQ, SWS, LOGN>(P, src, dst, batch, xcd_remap(blockIdx.x, nwg), SWA, lds, threadIdx.x);
+#endif
 }
 
 // ---------------------------------------------------------------------------

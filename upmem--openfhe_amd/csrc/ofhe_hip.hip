@@ -664,7 +664,7 @@ static void launch_tcols(const PlanArgs& a, bool spq, int split, bool inv, const
     }
     const u32 nwg = batch * a.towers * (256 / TCOLS_W);
 #define LT(I, SP)                                                                                 \
-    hipLaunchKernelGGL((k_tcols<I, SP>), dim3(nwg), dim3(16 * TCOLS_W), 0, s, a, src, dst, batch, nwg, \
+    hipLaunchKernelGGL((k_tcols<I, SP>), dim3(nwg / OFHE_TCOLS_LOOP), dim3(16 * TCOLS_W), 0, s, a, src, dst, batch, nwg, \
                        SwSrc{nullptr, 0, 0, nullptr, 1, 0})
     if (inv) {
         if (spq) LT(true, true); else LT(true, false);
