@@ -841,6 +841,15 @@ static_assert(TCOLS_W == 16 || TCOLS_W == 32, "column tile width");
 // same 256-row sub-transforms on 512 columns (the twiddle index of stage m is
 // m + row / (256 / m) whatever the row length).
 constexpr u32 TCOLS_LDS_WORDS = 16 * 16 * TCOLS_W + 16 * 16;
+// OFHE_TCOLS_HALF: the inverse column pass transposes through half the LDS in
+// two passes (A/B knob), its kernel sized for OFHE_TCOLS_HALF_WAVES waves per SIMD
+#ifndef OFHE_TCOLS_HALF
+#define OFHE_TCOLS_HALF 0
+#endif
+#ifndef OFHE_TCOLS_HALF_WAVES
+#define OFHE_TCOLS_HALF_WAVES 5
+#endif
+constexpr u32 TCOLS_LDS_INV_WORDS = OFHE_TCOLS_HALF ? 8 * 16 * TCOLS_W : TCOLS_LDS_WORDS;
 #ifndef OFHE_TCOLS_LOOP
 #define OFHE_TCOLS_LOOP 1  // tiles per workgroup (diagnostic variant builds only)
 #endif
@@ -913,13 +922,41 @@ __device__ __forceinline__ void tcols_body(const PlanArgs& P, const u64* src, u6
 #pragma unroll
             for (int k = 0; k < 16; k++) b8[k] = false;
             inv_round16_b(v, b8, itw, 16 + h, M);
+            if (OFHE_TCOLS_HALF) {
+                // the transpose through half the LDS (8 W x 16 words) in two
+                // passes: writers h < 8, then h >= 8 (wave-uniform), every
+                // thread reading 8 values per pass; 16 KiB per workgroup lets
+                // more workgroups share a CU (A/B knob)
+                u64 o[16];
+                if (h < 8) {
 #pragma unroll
-            for (int k = 0; k < 16; k++) lds[L2 + W * k] = v[k];
-            __syncthreads();
+                    for (int k = 0; k < 16; k++) lds[L2 + W * k] = v[k];
+                }
+                __syncthreads();
 #pragma unroll
-            for (int k = 0; k < 16; k++) {
-                v[k] = lds[L1 + 16 * W * k];
-                b8[k] = true;
+                for (int k = 0; k < 8; k++) o[k] = lds[L1 + 16 * W * k];
+                __syncthreads();
+                if (h >= 8) {
+#pragma unroll
+                    for (int k = 0; k < 16; k++) lds[L2 - 8 * 16 * W + W * k] = v[k];
+                }
+                __syncthreads();
+#pragma unroll
+                for (int k = 8; k < 16; k++) o[k] = lds[L1 + 16 * W * (k - 8)];
+#pragma unroll
+                for (int k = 0; k < 16; k++) {
+                    v[k] = o[k];
+                    b8[k] = true;
+                }
+            } else {
+#pragma unroll
+                for (int k = 0; k < 16; k++) lds[L2 + W * k] = v[k];
+                __syncthreads();
+#pragma unroll
+                for (int k = 0; k < 16; k++) {
+                    v[k] = lds[L1 + 16 * W * k];
+                    b8[k] = true;
+                }
             }
             inv_round16_b(v, b8, itw, 1, M);
 #pragma unroll
@@ -940,10 +977,10 @@ __device__ __forceinline__ void tcols_body(const PlanArgs& P, const u64* src, u6
 }
 
 template <bool INV, bool SPQ, bool SWS = false, int LOGN = 16>
-__global__ __launch_bounds__(16 * TCOLS_W, OFHE_KB_WAVES) void k_tcols(PlanArgs P, const u64* src, u64* dst,
-                                                                       u32 batch, u32 nwg, SwSrc SWA) {
+__global__ __launch_bounds__(16 * TCOLS_W, (INV && OFHE_TCOLS_HALF) ? OFHE_TCOLS_HALF_WAVES : OFHE_KB_WAVES) void k_tcols(
+    PlanArgs P, const u64* src, u64* dst, u32 batch, u32 nwg, SwSrc SWA) {
     OFHE_VGPR_FLOOR();
-    __shared__ u64 lds[TCOLS_LDS_WORDS];
+    __shared__ u64 lds[INV ? TCOLS_LDS_INV_WORDS : TCOLS_LDS_WORDS];
 #if OFHE_TCOLS_LOOP > 1
     // diagnostic (persistent-loop cost): each workgroup runs OFHE_TCOLS_LOOP
     // tiles back to back, the grid shrunk by that factor (N = 2^16 launches)
