@@ -367,16 +367,20 @@ def test_keyswitch_bootstrap_shape(hip):
     (48, 16, 3, False, 1, ((48, 0),), "0"),           # the unfused kernels (OFHE_BCONV_COLS=0)
     (12, 4, 3, False, 1, ((12, 0), (12, 65537), (11, 0)), "1"),
     (8, 4, 2, True, 2, ((8, 0), (7, 65537)), "1"),     # generic moduli: Mod<false>, no special-prime fold
+    (10, 6, 4, False, 1, ((10, 0), (10, 3)), "1"),     # digits of 3 / 3 / 3 / 1 towers, 6 special towers
 ])
-def test_keyswitch_bconv_cols(hip, monkeypatch, sq, sp, dnum, generic, B, cases, fused):
+@pytest.mark.parametrize("icol", ["0", "1"])
+def test_keyswitch_bconv_cols(hip, monkeypatch, sq, sp, dnum, generic, B, cases, fused, icol):
     """N = 2^17 KeySwitchCore with ApproxSwitchCRTBasis fused with the targets'
     forward column pass (k_bconv_cols, the default) in ModUp (full level) and
     ModDown (t = 0), and with OFHE_BCONV_COLS=0, bit-exact against the oracle;
-    lower levels and t > 0 take the unfused kernels in the same call."""
+    lower levels and t > 0 take the unfused kernels in the same call.  icol = 1
+    (OFHE_KS_ICOL) also moves the sources' INTT column pass into k_bconv_cols."""
     H, ctx = hip
     import torch
 
     monkeypatch.setenv("OFHE_BCONV_COLS", fused)
+    monkeypatch.setenv("OFHE_KS_ICOL", icol)
     n, q, rq, p, rp, kp, ks = _ks_case(H, ctx, 17, sq, sp, dnum, generic)
     rng = np.random.default_rng(1700 + sq)
     kb = _uniform(rng, dnum, q + p, n)

@@ -40,9 +40,78 @@ constexpr u32 BC_WAVES = OFHE_BCC_WAVES;
 constexpr u32 BC_THREADS = 64 * BC_WAVES;
 constexpr u32 BC_COLS = 16, BC_ROWS = 32, BC_POS = BC_COLS * BC_ROWS;
 
-template <int KS, bool SPQ>
+// ICOL: the sources arrive as the inverse block pass's output (the first 12
+// of the 17 inverse stages, lazy [0, 4q)), and the workgroup runs the last 5
+// -- the inverse column pass, GS on the columns {c + 4096 k} it owns -- before
+// the conversion, so the INTT's column pass (k_cols<5, inverse>) and its HBM
+// round trip disappear.  One wave per source tower (its modulus wave-uniform):
+// lane (qq, col) holds rows 8 qq .. 8 qq + 7 of column col; stages with row
+// distance 1, 2, 4 are in-lane, 8 and 16 cross lanes (xor 16, xor 32), each
+// partner computing 4 whole butterflies as in the target column pass below.
+// Every butterfly keeps its inputs < 8q (gs_bfly_b with in8), and the
+// conversion's Shoup product takes the lazy value: the same residue.
+// src_rel: plan tower of source 0 relative to P's first tower.
+template <bool SPQ>
+__device__ __forceinline__ void bcc_icol_source(const BconvArgs& A, const PlanArgs& P, const u64* __restrict__ xb,
+                                                u32 src, u32 src_rel, u32 lane, u64* dg64) {
+    constexpr u32 N = 1u << 17, COLS = N / BC_ROWS;
+    const u32 col = lane & 15, qq = lane >> 4;
+    const u32 ts = src_rel + src;
+    const auto M = load_mod<SPQ, (bool)OFHE_QA_CI>(P.tc[ts]);
+    const u64* itw = P.itw + (u64)ts * N * 2;
+    const u64* xs = xb + (u64)src * N + col;
+    u64 v[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++) v[k] = ld_s(xs + (u64)(8 * qq + k) * COLS);
+    // stage row distance 1: pairs (2j, 2j + 1), twiddle 16 + 4 qq + j
+#pragma unroll
+    for (int j = 0; j < 4; j++) gs_bfly_b(v[2 * j], v[2 * j + 1], ldtw(itw, 16 + 4 * qq + j), M, true);
+    // distance 2: pairs (4j + i, 4j + i + 2), twiddle 8 + 2 qq + j
+#pragma unroll
+    for (int j = 0; j < 2; j++) {
+        const Tw w = ldtw(itw, 8 + 2 * qq + j);
+#pragma unroll
+        for (int i = 0; i < 2; i++) gs_bfly_b(v[4 * j + i], v[4 * j + i + 2], w, M, true);
+    }
+    // distance 4: pairs (i, i + 4), twiddle 4 + qq
+    {
+        const Tw w = ldtw(itw, 4 + qq);
+#pragma unroll
+        for (int i = 0; i < 4; i++) gs_bfly_b(v[i], v[i + 4], w, M, true);
+    }
+    // distance 8 (lanes qq, qq ^ 1) then 16 (qq, qq ^ 2): the lower lane keeps
+    // butterflies 0..3, the upper 4..7; afterwards v[m] / v[4 + m] hold rows
+    // base + m / base + step + m
+    auto cross = [&](u32 xmask, const Tw w, bool upper) {
+#pragma unroll
+        for (int m = 0; m < 4; m++) {
+            const u64 snd = upper ? v[m] : v[4 + m];
+            const u64 rcv = pack((u32)__shfl_xor((int)lo32(snd), (int)xmask), (u32)__shfl_xor((int)hi32(snd), (int)xmask));
+            u64 xv = upper ? rcv : v[m];
+            u64 yv = upper ? v[4 + m] : rcv;
+            gs_bfly_b(xv, yv, w, M, true);
+            v[m] = xv;
+            v[4 + m] = yv;
+        }
+    };
+    cross(16, ldtw(itw, 2 + (qq >> 1)), qq & 1);
+    cross(32, ldtw(itw, 1), (qq >> 1) & 1);
+    // rows: v[m] -> 4 (qq & 1) + 8 (qq >> 1) + m, v[4 + m] -> that + 16
+    const BmSrc S = reinterpret_cast<const BmSrc*>(reinterpret_cast<const unsigned char*>(A.mm_tab) +
+                                                   (size_t)A.mm_tiles * A.mm_ks * 1024 + 4 * A.mm_tiles * sizeof(BmRed))[src];
+    const u32 r0 = 4 * (qq & 1) + 8 * (qq >> 1);
+    const u32 pr = src >> 1, hv = src & 1;
+#pragma unroll
+    for (int m = 0; m < 8; m++) {
+        const u32 row = r0 + (m & 3) + (m >= 4 ? 16 : 0);
+        const u64 y = shoup_canon(v[m], S.w, S.wp, S.q);
+        dg64[2 * ((u64)pr * BC_POS + row * BC_COLS + col) + hv] = digits8(y);
+    }
+}
+
+template <int KS, bool SPQ, bool ICOL = false>
 __global__ __launch_bounds__(BC_THREADS, OFHE_BCC_MINW) void k_bconv_cols(BconvArgs A, PlanArgs P, const u64* __restrict__ x,
-                                                           u64* __restrict__ out, u32 batch, u32 nwg) {
+                                                           u64* __restrict__ out, u32 batch, u32 nwg, u32 src_rel) {
     OFHE_VGPR_FLOOR();
     static_assert(KS >= 1 && KS <= 4, "k_bconv_cols: up to 16 source towers (64 KiB of digits)");
     constexpr u32 N = 1u << 17, COLS = N / BC_ROWS;
@@ -56,7 +125,23 @@ __global__ __launch_bounds__(BC_THREADS, OFHE_BCC_MINW) void k_bconv_cols(BconvA
     const i32x4* frag = reinterpret_cast<const i32x4*>(tab);                                    // [tiles][KS][64]
     const BmRed* red = reinterpret_cast<const BmRed*>(tab + (size_t)tiles * KS * 1024);        // [4 tiles]
     const BmSrc* srcc = reinterpret_cast<const BmSrc*>(red + 4 * tiles);                       // [4 KS]
-    {
+    if (ICOL) {
+        // 1'. the sources' inverse column pass and digits, one wave per source
+        u64* dg64 = reinterpret_cast<u64*>(dg);
+        const u64* xb = x + (u64)b * A.in_stride + c0;
+#pragma unroll 1
+        for (u32 src = w; src < 4 * KS; src += BC_WAVES) {
+            if (src < A.size_q) {
+                bcc_icol_source<SPQ>(A, P, xb, src, src_rel, lane, dg64);
+            } else {
+#pragma unroll
+                for (int m = 0; m < 8; m++) {
+                    const u32 row = 8 * (lane >> 4) + m;
+                    dg64[2 * ((u64)(src >> 1) * BC_POS + row * BC_COLS + (lane & 15)) + (src & 1)] = 0;
+                }
+            }
+        }
+    } else {
         // 1. digits of the sources, two per 16-byte slot (the lane's B operand);
         // every load of the thread goes out before the first product
         constexpr u32 ITEMS = 2 * KS * BC_POS, PER = (ITEMS + BC_THREADS - 1) / BC_THREADS;

@@ -88,8 +88,18 @@ int plan_ntt_fwd_sub(ofhe_plan_t p, u32 t0, u32 count, u64* y, u64 ystride, cons
 // Target j is written (column-pass output, the block pass's input) at tower
 // j (+ B.gap from B.gap_at on) of `out`, transformed with plan tower t0 + that
 // index.  bconv_cols_ok says whether it applies.
+// src_t0 >= 0: x holds the sources' inverse BLOCK pass output (plan towers
+// src_t0 .. src_t0 + B.size_q - 1, plan_ntt_inv_block) and the kernel runs
+// their inverse column pass itself before converting.
 bool bconv_cols_ok(ofhe_plan_t p, const BconvArgs& B);
-int bconv_cols_run(ofhe_plan_t p, u32 t0, const BconvArgs& B, const u64* x, u64* out, u32 batch, hipStream_t s);
+int bconv_cols_run(ofhe_plan_t p, u32 t0, const BconvArgs& B, const u64* x, u64* out, u32 batch, hipStream_t s,
+                   int src_t0 = -1);
+
+// The inverse transform's first pass only (the block pass, log_n > 12): the
+// column pass that completes it is left to the consumer (k_bconv_cols with
+// src_t0 >= 0).
+int plan_ntt_inv_block(ofhe_plan_t p, u32 t0, u32 count, const u64* src, u64 sstride, u64* dst, u64 dstride, u32 batch,
+                       hipStream_t s);
 
 // Forward column pass (2^12 < N; not SPLIT_T9) of the towers
 // lifted from `last` ([batch] rows of N, stride lstride, modulus ql; first

@@ -117,7 +117,13 @@ struct ModDownArgs {
     const TowerScalar* tinv_p;     // [size_p] or NULL (t = 0)
     const TowerScalar* t_q;        // [size_q] or NULL
     bool bcols = false;            // k_bconv_cols for the conversion + column pass when it applies
+    bool icol = false;             // ... also fed by the P part's inverse block pass (plan_p == plan_q)
 };
+// k_bconv_cols also runs the sources' inverse column pass (the INTT's second
+// pass) when they come from the same plan and nothing scales them in between
+static bool md_icol(const ModDownArgs& A) {
+    return A.bcols && A.icol && !A.t_q && !A.tinv_p && A.plan_p == A.plan_q && A.plan_q->log_n == 17;
+}
 
 int mod_down_run(const ModDownArgs& A, const u64* x, u64 xstride, u64* out, u64 ostride, u32 batch, hipStream_t s) {
     const u32 log_n = A.plan_q->log_n;
@@ -126,6 +132,21 @@ int mod_down_run(const ModDownArgs& A, const u64* x, u64 xstride, u64* out, u64 
     RCCHK(sp.alloc((size_t)batch * A.size_p * N * 8, s, A.plan_q->ctx));
     RCCHK(sq.alloc((size_t)batch * A.size_q * N * 8, s, A.plan_q->ctx));
     const u64 ps = A.size_p * N, qs = A.size_q * N;
+    if (md_icol(A)) {
+        BconvArgs B = A.bconv;
+        B.in_stride = ps;
+        B.out_stride = qs;
+        B.gap_at = A.size_q;
+        B.gap = 0;
+        B.lazy_out = 1;
+        if (bconv_cols_ok(A.plan_q, B)) {
+            // partP's INTT: its block pass here, its column pass inside the conversion
+            RCCHK(plan_ntt_inv_block(A.plan_p, A.p0, A.size_p, x + qs, xstride, sp.w(), ps, batch, s));
+            RCCHK(bconv_cols_run(A.plan_q, A.q0, B, sp.w(), sq.w(), batch, s, (int)A.p0));
+            return plan_ntt_fwd_sub(A.plan_q, A.q0, A.size_q, sq.w(), qs, x, xstride, out, ostride,
+                                    reinterpret_cast<const u64*>(A.pinv), batch, s, 2);
+        }
+    }
     // partP: P towers to coefficient form (dcrtpoly-impl.h:1147-1153)
     RCCHK(plan_ntt_range(A.plan_p, true, A.p0, A.size_p, x + qs, sp.w(), xstride, ps, batch, s));
     if (A.tinv_p) RCCHK(scale_towers(A.tinv_p, sp.w(), sp.w(), ps, ps, batch, A.size_p, log_n, s));
@@ -167,20 +188,24 @@ int mod_down_run2(const ModDownArgs& A, const u64* x0, u64 xstride, u64* out0, u
     RCCHK(sp.alloc((size_t)b2 * A.size_p * N * 8, s, A.plan_q->ctx));
     RCCHK(sq.alloc((size_t)b2 * A.size_q * N * 8, s, A.plan_q->ctx));
     const u64 ps = A.size_p * N, qs = A.size_q * N;
-    RCCHK(plan_ntt_range(A.plan_p, true, A.p0, A.size_p, x0 + qs, sp.w(), xstride, ps, b2, s));
-    if (A.tinv_p) RCCHK(scale_towers(A.tinv_p, sp.w(), sp.w(), ps, ps, b2, A.size_p, log_n, s));
     BconvArgs B = A.bconv;
     B.in_stride = ps;
     B.out_stride = qs;
     B.gap_at = A.size_q;
     B.gap = 0;
     B.lazy_out = 1;  // a forward NTT (after an optional tower scale) follows
+    const bool icol = md_icol(A) && bconv_cols_ok(A.plan_q, B);
+    if (icol)  // partP's INTT: its block pass here, its column pass inside the conversion
+        RCCHK(plan_ntt_inv_block(A.plan_p, A.p0, A.size_p, x0 + qs, xstride, sp.w(), ps, b2, s));
+    else
+        RCCHK(plan_ntt_range(A.plan_p, true, A.p0, A.size_p, x0 + qs, sp.w(), xstride, ps, b2, s));
+    if (A.tinv_p) RCCHK(scale_towers(A.tinv_p, sp.w(), sp.w(), ps, ps, b2, A.size_p, log_n, s));
     const u64* x1 = x0 + (u64)batch * xstride;
     u64* sq1 = sq.w() + (u64)batch * qs;
     const u64* pinv = reinterpret_cast<const u64*>(A.pinv);
     if (A.bcols && !A.t_q && bconv_cols_ok(A.plan_q, B)) {
         // the conversion writes the Q towers' column-pass output directly
-        RCCHK(bconv_cols_run(A.plan_q, A.q0, B, sp.w(), sq.w(), b2, s));
+        RCCHK(bconv_cols_run(A.plan_q, A.q0, B, sp.w(), sq.w(), b2, s, icol ? (int)A.p0 : -1));
         RCCHK(plan_ntt_fwd_sub(A.plan_q, A.q0, A.size_q, sq.w(), qs, x0, xstride, out0, ostride, pinv, batch, s, 2));
         return plan_ntt_fwd_sub(A.plan_q, A.q0, A.size_q, sq1, qs, x1, xstride, out1, ostride, pinv, batch, s, 2);
     }
@@ -305,6 +330,7 @@ struct ofhe_ks_s {
     hipStream_t side[KS_NSIDE] = {};  // fork streams (OFHE_KS_STREAMS=1: none)
     u32 chunk = 0;                    // ciphertexts per ModUp chunk (OFHE_KS_CHUNK; 0: the whole batch)
     bool bcols = true;                // k_bconv_cols in ModUp / ModDown (OFHE_BCONV_COLS=0: off)
+    bool icol = false;                // ... with the INTT's column pass inside it (OFHE_KS_ICOL)
     std::mutex mu;
     std::map<u32, KsLevel*> levels;
 };
@@ -354,6 +380,8 @@ int ofhe_hip_ks_create(ofhe_ctx_t ctx, uint32_t log_n, uint32_t size_q, const ui
     k->plan = plan;
     const char* bcc = getenv("OFHE_BCONV_COLS");  // k_bconv_cols (default on; 0: separate kernels, A/B)
     k->bcols = !(bcc && atoi(bcc) == 0);          // read per engine, so tests can switch it
+    const char* ic = getenv("OFHE_KS_ICOL");
+    k->icol = ic && atoi(ic) != 0;
     const char* ck = getenv("OFHE_KS_CHUNK");
     if (ck) k->chunk = (u32)atoi(ck);
     const char* ns = getenv("OFHE_KS_STREAMS");
@@ -563,18 +591,23 @@ static int ks_precompute_impl(ofhe_ks_t k, KsLevel* L, uint32_t size_ql, const u
         hipStream_t s = fk.f[j % KS_NSIDE];  // digits are independent
         u64* slot = digits + (u64)b0 * ds + j * poly;
         const uint64_t* c_ = c + (u64)b0 * l * N;
-        // partsCt[j] in coefficient form (keyswitch-hybrid.cpp:384-385)
-        RCCHK(plan_ntt_range(k->plan, true, st, n, c_ + st * N, slot + st * N, l * N, ds, batch_, s));
         // ApproxSwitchCRTBasis to the complement, written around the digit slot (388-406)
         BconvArgs B = L->up[j]->args;
         B.in_stride = B.out_stride = ds;
         B.gap_at = st;
         B.gap = n;
         B.lazy_out = 1;  // every complement tower goes through a forward NTT below
-        if (k->bcols && l == k->size_q && bconv_cols_ok(k->plan, B)) {
+        const bool cols = k->bcols && l == k->size_q && bconv_cols_ok(k->plan, B);
+        // partsCt[j] in coefficient form (keyswitch-hybrid.cpp:384-385); with
+        // k->icol only its block pass here, its column pass inside the conversion
+        if (cols && k->icol)
+            RCCHK(plan_ntt_inv_block(k->plan, st, n, c_ + st * N, l * N, slot + st * N, ds, batch_, s));
+        else
+            RCCHK(plan_ntt_range(k->plan, true, st, n, c_ + st * N, slot + st * N, l * N, ds, batch_, s));
+        if (cols) {
             // full level (slot towers = plan towers): the conversion writes the
             // complement's column-pass output, the block passes finish it (394)
-            RCCHK(bconv_cols_run(k->plan, 0, B, slot + st * N, slot, batch_, s));
+            RCCHK(bconv_cols_run(k->plan, 0, B, slot + st * N, slot, batch_, s, k->icol ? (int)st : -1));
             if (st) RCCHK(plan_ntt_fwd_block(k->plan, 0, st, slot, ds, batch_, s));
             RCCHK(plan_ntt_fwd_block(k->plan, st + n, (u32)(l + P) - st - n, slot + (st + n) * N, ds, batch_, s));
             if (own_copy) RCCHK(copy_rows(slot + st * N, ds, c_ + st * N, l * N, (u64)n * N, batch_, s));
@@ -659,7 +692,7 @@ static int ks_mod_down_impl(ofhe_ks_t k, KsLevel* L, const u64* x, u64* out, u64
     if (t) RCCHK(level_t_tables(k, L, t, &tt));
     const u32 l = L->size_ql, P = k->size_p;
     ModDownArgs A{k->plan, k->plan, 0, k->size_q, l, P, L->down->args, L->d_pinv,
-                  tt ? tt : nullptr, tt ? tt + P : nullptr, k->bcols};
+                  tt ? tt : nullptr, tt ? tt + P : nullptr, k->bcols, k->icol};
     const u64 N = 1ull << k->log_n;
     return mod_down_run(A, x, (u64)(l + P) * N, out, (u64)l * N, batch, s);
 }
@@ -697,7 +730,7 @@ int ofhe_hip_ks_core(ofhe_ks_t k, uint32_t size_ql, const uint64_t* c, const uin
         if (t) RCCHK(level_t_tables(k, L, t, &tt));
         const u32 l = L->size_ql, P = k->size_p;
         ModDownArgs A{k->plan, k->plan, 0, k->size_q, l, P, L->down->args, L->d_pinv,
-                      tt ? tt : nullptr, tt ? tt + P : nullptr, k->bcols};
+                      tt ? tt : nullptr, tt ? tt + P : nullptr, k->bcols, k->icol};
         return mod_down_run2(A, c0, poly, out0, out1, (u64)l * N, batch, s);
     }
     KsFork fk;  // after dg, ct: joins before they are freed

@@ -785,6 +785,20 @@ int plan_ntt_fwd_block(ofhe_plan_t p, u32 t0, u32 count, u64* y, u64 ystride, u3
     return post_launch();
 }
 
+int plan_ntt_inv_block(ofhe_plan_t p, u32 t0, u32 count, const u64* src, u64 sstride, u64* dst, u64 dstride, u32 batch,
+                       hipStream_t s) {
+    if (!p || !p->ctx) return fail(OFHE_ERR_STATE, "plan is NULL or destroyed");
+    if (p->log_n <= 12) return fail(OFHE_ERR_ARG, "plan_ntt_inv_block: log_n > 12 only");
+    if (count == 0 || batch == 0) return OFHE_OK;
+    if (t0 + count > p->towers) return fail(OFHE_ERR_ARG, "tower range outside the plan");
+    HIPCHK(hipSetDevice(p->ctx->device));
+    PlanArgs a = args_of(p, t0, count);
+    a.sstride = sstride;
+    a.dstride = dstride;
+    launch_block<MODE_INV>(a, p->spq, src, dst, nullptr, batch, s, p->split);
+    return post_launch();
+}
+
 int plan_ntt_fwd_sub(ofhe_plan_t p, u32 t0, u32 count, u64* y, u64 ystride, const u64* x, u64 xstride, u64* out,
                      u64 ostride, const u64* scal, u32 batch, hipStream_t s, int parts) {
     if (!p || !p->ctx) return fail(OFHE_ERR_STATE, "plan is NULL or destroyed");
@@ -1517,8 +1531,12 @@ bool bconv_cols_ok(ofhe_plan_t p, const BconvArgs& B) {
            B.mm_ks >= 1 && B.mm_ks <= 4 && (B.mm_spq != 0) == p->spq;
 }
 
-int bconv_cols_run(ofhe_plan_t p, u32 t0, const BconvArgs& B, const u64* x, u64* out, u32 batch, hipStream_t s) {
+int bconv_cols_run(ofhe_plan_t p, u32 t0, const BconvArgs& B, const u64* x, u64* out, u32 batch, hipStream_t s,
+                   int src_t0) {
     if (!bconv_cols_ok(p, B)) return fail(OFHE_ERR_ARG, "internal: k_bconv_cols does not apply");
+    if (src_t0 >= 0 && ((u32)src_t0 < t0 || (u32)src_t0 + B.size_q > p->towers))
+        return fail(OFHE_ERR_ARG, "internal: k_bconv_cols sources outside the plan");
+    const u32 src_rel = src_t0 >= 0 ? (u32)src_t0 - t0 : 0;
     // the last target's plan tower (after the output gap) must exist
     const u64 last = (u64)B.size_p - 1 + (B.size_p - 1 >= B.gap_at ? B.gap : 0);
     if (t0 + last >= p->towers) return fail(OFHE_ERR_ARG, "internal: k_bconv_cols targets outside the plan");
@@ -1526,17 +1544,19 @@ int bconv_cols_run(ofhe_plan_t p, u32 t0, const BconvArgs& B, const u64* x, u64*
     if (nwg >= (1ull << 31)) return fail(OFHE_ERR_ARG, "batch too large");
     const PlanArgs a = args_of(p, t0);
     switch (B.mm_ks) {
-#define BCC(K)                                                                                                   \
-    case K:                                                                                                      \
-        if (p->spq)                                                                                              \
-            hipLaunchKernelGGL((k_bconv_cols<K, true>), dim3((u32)nwg), dim3(BC_THREADS), 0, s, B, a, x, out,   \
-                               batch, (u32)nwg);                                                                 \
-        else                                                                                                     \
-            hipLaunchKernelGGL((k_bconv_cols<K, false>), dim3((u32)nwg), dim3(BC_THREADS), 0, s, B, a, x, out,  \
-                               batch, (u32)nwg);                                                                 \
+#define BCC1(K, SP, IC) \
+    hipLaunchKernelGGL((k_bconv_cols<K, SP, IC>), dim3((u32)nwg), dim3(BC_THREADS), 0, s, B, a, x, out, batch, (u32)nwg, src_rel)
+#define BCC(K)                                                   \
+    case K:                                                      \
+        if (p->spq) {                                            \
+            if (src_t0 >= 0) BCC1(K, true, true); else BCC1(K, true, false); \
+        } else {                                                 \
+            if (src_t0 >= 0) BCC1(K, false, true); else BCC1(K, false, false); \
+        }                                                        \
         break;
         BCC(1) BCC(2) BCC(3) BCC(4)
 #undef BCC
+#undef BCC1
         default: break;
     }
     return post_launch();
