@@ -48,7 +48,7 @@ constexpr u32 BC_COLS = 16, BC_ROWS = 32, BC_POS = BC_COLS * BC_ROWS;
 // lane (qq, col) holds rows 8 qq .. 8 qq + 7 of column col; stages with row
 // distance 1, 2, 4 are in-lane, 8 and 16 cross lanes (xor 16, xor 32), each
 // partner computing 4 whole butterflies as in the target column pass below.
-// Every butterfly keeps its inputs < 8q (gs_bfly_b with in8), and the
+// Values stay below 8q (the lazy-GS bounds of cols_inv_b), and the
 // conversion's Shoup product takes the lazy value: the same residue.
 // src_rel: plan tower of source 0 relative to P's first tower.
 template <bool SPQ>
@@ -63,21 +63,31 @@ __device__ __forceinline__ void bcc_icol_source(const BconvArgs& A, const PlanAr
     u64 v[8];
 #pragma unroll
     for (int k = 0; k < 8; k++) v[k] = ld_s(xs + (u64)(8 * qq + k) * COLS);
+    // compile-time bounds per register as in cols_inv_b (b8: < 8q, else < 4q;
+    // a GS sum leaves < 8q, a Shoup difference < 4q): inputs < 4q
+    bool b8[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++) b8[k] = false;
+    auto bf = [&](int i, int j, const Tw w) {
+        gs_bfly_b(v[i], v[j], w, M, b8[i] || b8[j]);
+        b8[i] = true;
+        b8[j] = false;
+    };
     // stage row distance 1: pairs (2j, 2j + 1), twiddle 16 + 4 qq + j
 #pragma unroll
-    for (int j = 0; j < 4; j++) gs_bfly_b(v[2 * j], v[2 * j + 1], ldtw(itw, 16 + 4 * qq + j), M, true);
+    for (int j = 0; j < 4; j++) bf(2 * j, 2 * j + 1, ldtw(itw, 16 + 4 * qq + j));
     // distance 2: pairs (4j + i, 4j + i + 2), twiddle 8 + 2 qq + j
 #pragma unroll
     for (int j = 0; j < 2; j++) {
         const Tw w = ldtw(itw, 8 + 2 * qq + j);
 #pragma unroll
-        for (int i = 0; i < 2; i++) gs_bfly_b(v[4 * j + i], v[4 * j + i + 2], w, M, true);
+        for (int i = 0; i < 2; i++) bf(4 * j + i, 4 * j + i + 2, w);
     }
     // distance 4: pairs (i, i + 4), twiddle 4 + qq
     {
         const Tw w = ldtw(itw, 4 + qq);
 #pragma unroll
-        for (int i = 0; i < 4; i++) gs_bfly_b(v[i], v[i + 4], w, M, true);
+        for (int i = 0; i < 4; i++) bf(i, i + 4, w);
     }
     // distance 8 (lanes qq, qq ^ 1) then 16 (qq, qq ^ 2): the lower lane keeps
     // butterflies 0..3, the upper 4..7; afterwards v[m] / v[4 + m] hold rows
@@ -89,9 +99,12 @@ __device__ __forceinline__ void bcc_icol_source(const BconvArgs& A, const PlanAr
             const u64 rcv = pack((u32)__shfl_xor((int)lo32(snd), (int)xmask), (u32)__shfl_xor((int)hi32(snd), (int)xmask));
             u64 xv = upper ? rcv : v[m];
             u64 yv = upper ? v[4 + m] : rcv;
-            gs_bfly_b(xv, yv, w, M, true);
+            // either partner's slot: the union of both bounds (partners share b8)
+            gs_bfly_b(xv, yv, w, M, b8[m] || b8[4 + m]);
             v[m] = xv;
             v[4 + m] = yv;
+            b8[m] = true;
+            b8[4 + m] = false;
         }
     };
     cross(16, ldtw(itw, 2 + (qq >> 1)), qq & 1);

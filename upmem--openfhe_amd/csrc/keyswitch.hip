@@ -330,7 +330,7 @@ struct ofhe_ks_s {
     hipStream_t side[KS_NSIDE] = {};  // fork streams (OFHE_KS_STREAMS=1: none)
     u32 chunk = 0;                    // ciphertexts per ModUp chunk (OFHE_KS_CHUNK; 0: the whole batch)
     bool bcols = true;                // k_bconv_cols in ModUp / ModDown (OFHE_BCONV_COLS=0: off)
-    bool icol = false;                // ... with the INTT's column pass inside it (OFHE_KS_ICOL)
+    bool icol = true;                 // ... with the INTT's column pass inside it (OFHE_KS_ICOL=0: off)
     std::mutex mu;
     std::map<u32, KsLevel*> levels;
 };
@@ -380,8 +380,8 @@ int ofhe_hip_ks_create(ofhe_ctx_t ctx, uint32_t log_n, uint32_t size_q, const ui
     k->plan = plan;
     const char* bcc = getenv("OFHE_BCONV_COLS");  // k_bconv_cols (default on; 0: separate kernels, A/B)
     k->bcols = !(bcc && atoi(bcc) == 0);          // read per engine, so tests can switch it
-    const char* ic = getenv("OFHE_KS_ICOL");
-    k->icol = ic && atoi(ic) != 0;
+    const char* ic = getenv("OFHE_KS_ICOL");  // default on; 0: the INTT's own column pass (A/B)
+    k->icol = !(ic && atoi(ic) == 0);
     const char* ck = getenv("OFHE_KS_CHUNK");
     if (ck) k->chunk = (u32)atoi(ck);
     const char* ns = getenv("OFHE_KS_STREAMS");
