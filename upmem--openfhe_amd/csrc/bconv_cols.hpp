@@ -52,7 +52,7 @@ constexpr u32 BC_COLS = 16, BC_ROWS = 32, BC_POS = BC_COLS * BC_ROWS;
 // conversion's Shoup product takes the lazy value: the same residue.
 // src_rel: plan tower of source 0 relative to P's first tower.
 template <bool SPQ>
-__device__ __forceinline__ void bcc_icol_source(const BconvArgs& A, const PlanArgs& P, const u64* __restrict__ xb,
+__device__ __forceinline__ void bcc_icol_source(const PlanArgs& P, const BmSrc* srcc, const u64* __restrict__ xb,
                                                 u32 src, u32 src_rel, u32 lane, u64* dg64) {
     constexpr u32 N = 1u << 17, COLS = N / BC_ROWS;
     const u32 col = lane & 15, qq = lane >> 4;
@@ -110,8 +110,7 @@ __device__ __forceinline__ void bcc_icol_source(const BconvArgs& A, const PlanAr
     cross(16, ldtw(itw, 2 + (qq >> 1)), qq & 1);
     cross(32, ldtw(itw, 1), (qq >> 1) & 1);
     // rows: v[m] -> 4 (qq & 1) + 8 (qq >> 1) + m, v[4 + m] -> that + 16
-    const BmSrc S = reinterpret_cast<const BmSrc*>(reinterpret_cast<const unsigned char*>(A.mm_tab) +
-                                                   (size_t)A.mm_tiles * A.mm_ks * 1024 + 4 * A.mm_tiles * sizeof(BmRed))[src];
+    const BmSrc S = srcc[src];
     const u32 r0 = 4 * (qq & 1) + 8 * (qq >> 1);
     const u32 pr = src >> 1, hv = src & 1;
 #pragma unroll
@@ -145,7 +144,7 @@ __global__ __launch_bounds__(BC_THREADS, OFHE_BCC_MINW) void k_bconv_cols(BconvA
 #pragma unroll 1
         for (u32 src = w; src < 4 * KS; src += BC_WAVES) {
             if (src < A.size_q) {
-                bcc_icol_source<SPQ>(A, P, xb, src, src_rel, lane, dg64);
+                bcc_icol_source<SPQ>(P, srcc, xb, src, src_rel, lane, dg64);
             } else {
 #pragma unroll
                 for (int m = 0; m < 8; m++) {
