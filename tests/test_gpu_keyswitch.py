@@ -368,6 +368,7 @@ def test_keyswitch_bootstrap_shape(hip):
     (12, 4, 3, False, 1, ((12, 0), (12, 65537), (11, 0)), "1"),
     (8, 4, 2, True, 2, ((8, 0), (7, 65537)), "1"),     # generic moduli: Mod<false>, no special-prime fold
     (10, 6, 4, False, 1, ((10, 0), (10, 3)), "1"),     # digits of 3 / 3 / 3 / 1 towers, 6 special towers
+    (24, 12, 2, False, 1, ((24, 0),), "1"),            # 12-tower digits and P: the KS = 3 conversion kernels
 ])
 @pytest.mark.parametrize("icol", ["0", "1"])
 def test_keyswitch_bconv_cols(hip, monkeypatch, sq, sp, dnum, generic, B, cases, fused, icol):
