@@ -110,7 +110,8 @@ int ofhe_hip_plan_destroy(ofhe_plan_t plan);
  * in chunks of `chunk_batch` entries (0 = whole batch in one pass) and, with
  * streams = 2, alternate the chunks over two internal streams forked from and
  * joined back into the caller's stream.  Results are identical for any
- * setting; only speed changes. */
+ * setting; only speed changes.  Set it while no other thread launches with
+ * the same plan: the launches read the setting without taking the plan's lock. */
 int ofhe_hip_plan_tune(ofhe_plan_t plan, uint32_t chunk_batch, uint32_t streams);
 /* Performance knob for ofhe_hip_ntt_mul_intt at log_n = 16 (the SwitchFormat ->
  * Times -> SwitchFormat chain of dcrtpoly-impl.h:2518-2524 / dcrtpoly.h:185-200):
@@ -120,7 +121,8 @@ int ofhe_hip_plan_tune(ofhe_plan_t plan, uint32_t chunk_batch, uint32_t streams)
  * three launches.  Fails with OFHE_ERR_STATE when the plan cannot run it
  * (log_n != 16, or the device's workgroup placement did not pass the plan's
  * one-time XCD probe).  Chunking (ofhe_hip_plan_tune) takes precedence.
- * Results are identical either way. */
+ * Results are identical either way.  As for ofhe_hip_plan_tune, switch it
+ * while no other thread launches with the same plan. */
 int ofhe_hip_plan_pipeline(ofhe_plan_t plan, int persistent, uint32_t lag);
 /* Whether the persistent pipeline is selected, and how many of its waits gave
  * up since the plan was created (0 unless an invariant broke; the outputs of

@@ -124,9 +124,14 @@ __global__ __launch_bounds__(256, OFHE_KB_WAVES) void k_pipe(PlanArgs P, const u
     constexpr bool SC1 = HM == 1 || HM == 2;
     constexpr int OUT = (HM >= 2) ? 0 : 2;                  // IM bit 1: cached intermediate stores
     constexpr int IN = SC1 ? 4 : (HM == 3 ? 0 : 1);         // IM bits 0 / 2: plain or sc1 intermediate loads
-    // dynamic (C.wpq = 0): items from the queue head; static: the r-th
-    // workgroup of this XCD takes items r, r + wpq, r + 2 wpq, ... (no claim
-    // per item; deadlock-free too: the lowest unfinished item never waits)
+    // dynamic (C.wpq = 0): items from the queue head, handed only to running
+    // workgroups, so every wait ends whatever the residency.  Static
+    // (OFHE_PIPE_STATIC, an A/B knob): the r-th workgroup of this XCD takes
+    // items r, r + wpq, r + 2 wpq, ... with no claim per item; the lowest
+    // unfinished item never waits, so it completes as long as all wpq
+    // workgroups of the queue are resident (the grid is sized to that); a
+    // concurrent kernel holding CU slots can stall it until the bounded wait
+    // gives up, which err counts
     if (tid == 0) s_next = __hip_atomic_fetch_add(C.wpq ? C.members + PIPE_QSTRIDE * q : head, 1u, __ATOMIC_RELAXED,
                                                   __HIP_MEMORY_SCOPE_AGENT);
     __syncthreads();
