@@ -11,6 +11,10 @@ Two kinds of fixture live here:
      - UnitTestNTT.cpp:53-133 round-trip inputs
      - UnitTestPolyElements.cpp:265-305 SwitchModulus KAT, 500-523
        AutomorphismTransform KAT (q=73, m=8)
+     - UnitTestBFVrnsCRTOperations.cpp:290-376 FastExpandCRTBasisPloverQ KAT
+       (N = 8, two 60-bit towers): its P_l part is the ApproxSwitchCRTBasis
+       sum of dcrtpoly-impl.h:1419-1441 with the constants of
+       bfvrns-cryptoparameters.cpp:501-523
      - SURVEY.md §8(c) probe outputs (moduli, minimal roots, y[0], y[1], c[0][0])
 2. Oracle outputs (oracle/ofhe_oracle.c) at small sizes, used as committed
    golden vectors for the GPU parity tests (regenerate with this script; the
@@ -71,6 +75,30 @@ def reference_fixtures():
             "ref": "src/core/unittest/UnitTestPolyElements.cpp:500-523",
             "q": 73, "m": 8, "root": 22, "format": "coefficient",
             "x": [56, 1, 37, 2], "k": 3, "expected": [56, 2, 36, 1],
+        },
+        "kat_fast_expand_crt_basis": {
+            "ref": "src/pke/unittest/utbfvrns/UnitTestBFVrnsCRTOperations.cpp:290-376",
+            "op": "DCRTPolyImpl::FastExpandCRTBasisPloverQ (dcrtpoly-impl.h:1413-1466); its first loop "
+                  "(1419-1441) is ApproxSwitchCRTBasis from Q to R_l with x_i * (-R_l QHat_i^-1 mod q_i) "
+                  "(m_negRlQHatInvModq, bfvrns-cryptoparameters.cpp:501-515) and q_i^-1 mod r_j "
+                  "(m_qInvModr, 517-523)",
+            "m": 16,
+            "q": [1152921504606846577, 1152921504606846097],
+            "r": [1152921504606845777, 1152921504606845473],
+            "x": [[242947838436205858, 458804958636264704, 813208723994158017, 738376275125875131,
+                   269337450701982501, 633721177525656427, 406635995163024073, 763204304316606329],
+                  [1024863409567898083, 845721255474383902, 537504300724180111, 1018489837930110795,
+                   112800627588840746, 1119710169440476902, 77894506676832730, 34149187620514595]],
+            "expected_rl": [[955839852875274614, 186398073668078476, 710455872402389881, 1065981546244475424,
+                             1049296073052489283, 578396240339812092, 26954876970280156, 1019223053257416912],
+                            [874592295621923164, 585167928946466637, 612704504638527027, 551633899923050545,
+                             758002500979691774, 694035684451390662, 625796987487151016, 96319544173820807]],
+            "expected_ql_note": "towers 0-1 of the test's answer (ans0, ans1) come from the exact HPS "
+                                "SwitchCRTBasis (dcrtpoly-impl.h:1445-1447, floating-point alpha), not on the path",
+            "expected_ql": [[805568738929329616, 1078766251747424582, 785656076316475932, 599125608237504784,
+                             541576441836927290, 152721755350883626, 574857357780891061, 1081393409810468825],
+                            [434562805454153184, 312761043978375123, 509951653046700586, 879239171041671808,
+                             385039618723450975, 638710747265582661, 246115869294473638, 352338293114574371]],
         },
         "survey_probes": {
             "ref": "SURVEY.md §8(c) (reference native code run in the survey container)",

@@ -241,6 +241,32 @@ def test_base_conversion_golden(hip, O, case):
     assert host(out).reshape(-1).tolist() == c["out"]
 
 
+@pytest.mark.parametrize("log_n", [3, 5, 12, 17])
+def test_kat_fast_expand_crt_basis(hip, log_n):
+    """UnitTestBFVrnsCRTOperations.cpp:290-376 through the C ABI: the R_l towers
+    of FastExpandCRTBasisPloverQ's answer (its ApproxSwitchCRTBasis loop,
+    dcrtpoly-impl.h:1419-1441) with the test's constants; the N = 8 vectors
+    tiled to N = 2^log_n (the conversion is coefficient-wise) so the small-ring,
+    matrix-core and 2^17 kernels all see them; batch entry 1 holds the columns
+    reversed."""
+    import torch
+    from test_oracle import fast_expand_constants
+
+    H, ctx = hip
+    k = REF["kat_fast_expand_crt_basis"]
+    q, r = k["q"], k["r"]
+    c, d = fast_expand_constants(q, r)
+    reps = (1 << log_n) // 8
+    x0 = np.tile(np.array(k["x"], np.uint64), (1, reps))
+    want0 = np.tile(np.array(k["expected_rl"], np.uint64), (1, reps))
+    x = np.stack([x0, x0[:, ::-1]])
+    want = np.stack([want0, want0[:, ::-1]])
+    bc = H.BaseConverter(ctx, log_n, q, r, c, [v for row in d for v in row])
+    out = torch.zeros((2, len(r), 1 << log_n), dtype=torch.int64, device="cuda")
+    bc.switch(dev(x).data_ptr(), out.data_ptr(), 2, stream())
+    assert np.array_equal(host(out), want)
+
+
 def test_base_conversion_config5_shape(hip, O):
     """N = 2^17 digit -> complement (16 -> 17 towers), vs the oracle."""
     import torch

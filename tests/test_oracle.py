@@ -162,3 +162,35 @@ def test_golden_vectors_regenerate(O):
         b = O.U(c["b"]).reshape(B, T, n)
         assert O.ntt_fwd(a, tb).reshape(-1).tolist() == c["ntt_a"]
         assert O.ntt_mul_intt(a, b, tb).reshape(-1).tolist() == c["pipeline"]
+
+
+def fast_expand_constants(q, r):
+    """The BFVrns precomputations FastExpandCRTBasisPloverQ reads
+    (bfvrns-cryptoparameters.cpp:501-523), with Python big integers:
+    c_i = q_i - [R QHat_i^-1]_{q_i} (m_negRlQHatInvModq) and
+    d_ij = q_i^-1 mod r_j (m_qInvModr); Q and R are the products of q and r."""
+    Q = R = 1
+    for v in q:
+        Q *= v
+    for v in r:
+        R *= v
+    c = [qi - R * pow(Q // qi, -1, qi) % qi for qi in q]
+    d = [[pow(qi, -1, rj) for rj in r] for qi in q]
+    return c, d
+
+
+def test_kat_fast_expand_crt_basis(O):
+    """UnitTestBFVrnsCRTOperations.cpp:290-376: the R_l towers of
+    FastExpandCRTBasisPloverQ's answer are the base conversion of
+    dcrtpoly-impl.h:1419-1441 -- y_i = [x_i c_i]_{q_i} (Shoup), the 128-bit sum
+    of y_i d_ij, BarrettUint128ModUint64 -- i.e. ApproxSwitchCRTBasis with the
+    caller's constants in place of QHatInv / QHatModp."""
+    k = REF["kat_fast_expand_crt_basis"]
+    q, r = k["q"], k["r"]
+    c, d = fast_expand_constants(q, r)
+    pre = O.base_conv_precompute(q, r)
+    pre["qhinv"] = O.U(c)
+    pre["qhinv_pre"] = O.U([(ci << 64) // qi for ci, qi in zip(c, q)])  # PrepModMulConst
+    pre["qhmodp"] = O.U([v for row in d for v in row])
+    out = O.approx_switch_crt_basis(O.U(k["x"]), q, r, pre)
+    assert out.tolist() == k["expected_rl"]
