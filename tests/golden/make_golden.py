@@ -11,6 +11,10 @@ Two kinds of fixture live here:
      - UnitTestNTT.cpp:53-133 round-trip inputs
      - UnitTestPolyElements.cpp:265-305 SwitchModulus KAT, 500-523
        AutomorphismTransform KAT (q=73, m=8)
+     - UnitTestCommonElements.cpp:240-320 common_binary_ops and 381-446
+       common_arithmetic_ops_element (q=73, m=8): Plus / Minus / Times in
+       evaluation form, SwitchFormat -> Times -> SwitchFormat, scalar ops;
+       457-483 AddILElementOne
      - UnitTestBFVrnsCRTOperations.cpp:290-376 FastExpandCRTBasisPloverQ KAT
        (N = 8, two 60-bit towers): its P_l part is the ApproxSwitchCRTBasis
        sum of dcrtpoly-impl.h:1419-1441 with the constants of
@@ -75,6 +79,20 @@ def reference_fixtures():
             "ref": "src/core/unittest/UnitTestPolyElements.cpp:500-523",
             "q": 73, "m": 8, "root": 22, "format": "coefficient",
             "x": [56, 1, 37, 2], "k": 3, "expected": [56, 2, 36, 1],
+        },
+        "kat_common_elements": {
+            "ref": "src/core/unittest/UnitTestCommonElements.cpp:240-320, 381-446, 457-483",
+            "q": 73, "m": 8, "root": 22,
+            "binary_ops": {
+                "a": [2, 1, 1, 1], "b": [1, 0, 1, 1],
+                "plus_eval": [3, 1, 2, 2], "minus_eval": [1, 1, 0, 0], "times_eval": [2, 0, 1, 1],
+                "switchformat_times_switchformat": [0, 72, 2, 4],
+            },
+            "scalar_ops": {
+                "coef_x": [1, 3, 4, 1], "plus_1_coefficient_form": [2, 3, 4, 1],
+                "eval_x": [2, 1, 4, 1], "minus_1_eval": [1, 0, 3, 0], "times_2_eval": [4, 2, 8, 2],
+            },
+            "add_il_element_one": {"x": [2, 1, 3, 2], "expected": [3, 2, 4, 3]},
         },
         "kat_fast_expand_crt_basis": {
             "ref": "src/pke/unittest/utbfvrns/UnitTestBFVrnsCRTOperations.cpp:290-376",

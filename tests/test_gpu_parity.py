@@ -93,6 +93,53 @@ def test_kat_mubintvec(hip):
         assert host(c).tolist() == k["mod" + op], op
 
 
+def test_kat_common_elements(hip):
+    """UnitTestCommonElements.cpp (q = 73, N = 4) through the C ABI:
+    common_binary_ops (240-320) -- evaluation-form Plus / Minus / Times and
+    SwitchFormat -> Times -> SwitchFormat, here both as separate transforms and
+    as the fused pipeline; common_arithmetic_ops_element (381-446) -- Plus(1)
+    in coefficient form at coefficient 0 only, Minus(1) / Times(2) on every
+    slot; AddILElementOne (457-483)."""
+    import torch
+
+    H, ctx = hip
+    k = REF["kat_common_elements"]
+    plan = H.NTTPlan(ctx, 2, [k["q"]], [k["root"]])
+    vec = lambda v: dev(np.array(v, np.uint64).reshape(1, 1, 4))  # noqa: E731
+    flat = lambda t: host(t).reshape(-1).tolist()  # noqa: E731
+    bo = k["binary_ops"]
+    a, b = vec(bo["a"]), vec(bo["b"])
+    for op, key in (("add", "plus_eval"), ("sub", "minus_eval"), ("mul", "times_eval")):
+        c = torch.empty_like(a)
+        getattr(plan, "mod_" + op)(a.data_ptr(), b.data_ptr(), c.data_ptr(), 1, stream())
+        assert flat(c) == bo[key], op
+    fa, fb = vec(bo["a"]), vec(bo["b"])
+    plan.forward(fa.data_ptr(), 1, stream())
+    plan.forward(fb.data_ptr(), 1, stream())
+    c = torch.empty_like(fa)
+    plan.mod_mul(fa.data_ptr(), fb.data_ptr(), c.data_ptr(), 1, stream())
+    plan.inverse(c.data_ptr(), 1, stream())
+    assert flat(c) == bo["switchformat_times_switchformat"]
+    c2 = torch.empty_like(fa)
+    plan.ntt_mul_intt(a.data_ptr(), fb.data_ptr(), c2.data_ptr(), 1, stream())
+    assert flat(c2) == bo["switchformat_times_switchformat"]
+    so = k["scalar_ops"]
+    x = vec(so["coef_x"])
+    plan.mod_add_scalar_at(x.data_ptr(), 0, [1], x.data_ptr(), 1, stream())
+    assert flat(x) == so["plus_1_coefficient_form"]
+    e = vec(so["eval_x"])
+    c = torch.empty_like(e)
+    plan.mod_sub_scalar(e.data_ptr(), [1], c.data_ptr(), 1, stream())
+    assert flat(c) == so["minus_1_eval"]
+    plan.mod_mul_scalar(e.data_ptr(), [2], c.data_ptr(), 1, stream())
+    assert flat(c) == so["times_2_eval"]
+    one = k["add_il_element_one"]
+    x = vec(one["x"])
+    plan.mod_add_scalar(x.data_ptr(), [1], x.data_ptr(), 1, stream())
+    assert flat(x) == one["expected"]
+    plan.close()
+
+
 @pytest.mark.parametrize("case", range(5))
 def test_golden_vectors(hip, case):
     H, ctx = hip

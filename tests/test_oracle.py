@@ -194,3 +194,28 @@ def test_kat_fast_expand_crt_basis(O):
     pre["qhmodp"] = O.U([v for row in d for v in row])
     out = O.approx_switch_crt_basis(O.U(k["x"]), q, r, pre)
     assert out.tolist() == k["expected_rl"]
+
+
+def test_kat_common_elements(O):
+    """UnitTestCommonElements.cpp: common_binary_ops (240-320: evaluation-form
+    Plus / Minus / Times, and SwitchFormat -> Times -> SwitchFormat, i.e. the
+    negacyclic product), common_arithmetic_ops_element (381-446: Plus(1) in
+    coefficient form touches coefficient 0 only, Minus(1) / Times(2) every
+    slot) and AddILElementOne (457-483)."""
+    k = REF["kat_common_elements"]
+    q = [k["q"]]
+    vec = lambda v: O.U(v).reshape(1, 1, -1)  # noqa: E731
+    bo = k["binary_ops"]
+    a, b = vec(bo["a"]), vec(bo["b"])
+    assert O.eltwise("add", a, b, q).reshape(-1).tolist() == bo["plus_eval"]
+    assert O.eltwise("sub", a, b, q).reshape(-1).tolist() == bo["minus_eval"]
+    assert O.eltwise("mul", a, b, q).reshape(-1).tolist() == bo["times_eval"]
+    tb = O.Tables(k["m"] // 2, q, [k["root"]])
+    got = O.ntt_mul_intt(a, O.ntt_fwd(b, tb), tb)
+    assert got.reshape(-1).tolist() == bo["switchformat_times_switchformat"]
+    so = k["scalar_ops"]
+    assert O.add_scalar_at(vec(so["coef_x"]), 0, [1], q).reshape(-1).tolist() == so["plus_1_coefficient_form"]
+    assert O.sub_scalar(vec(so["eval_x"]), [1], q).reshape(-1).tolist() == so["minus_1_eval"]
+    assert O.mul_scalar(vec(so["eval_x"]), [2], q).reshape(-1).tolist() == so["times_2_eval"]
+    one = k["add_il_element_one"]
+    assert O.add_scalar(vec(one["x"]), [1], q).reshape(-1).tolist() == one["expected"]
