@@ -15,6 +15,8 @@ Two kinds of fixture live here:
        common_arithmetic_ops_element (q=73, m=8): Plus / Minus / Times in
        evaluation form, SwitchFormat -> Times -> SwitchFormat, scalar ops;
        457-483 AddILElementOne
+     - UnitTestNbTheory.cpp:165-186 FirstPrime KATs and 381-394 the NextPrime
+       chain (the moduli generation behind every plan)
      - UnitTestBFVrnsCRTOperations.cpp:290-376 FastExpandCRTBasisPloverQ KAT
        (N = 8, two 60-bit towers): its P_l part is the ApproxSwitchCRTBasis
        sum of dcrtpoly-impl.h:1419-1441 with the constants of
@@ -93,6 +95,14 @@ def reference_fixtures():
                 "eval_x": [2, 1, 4, 1], "minus_1_eval": [1, 0, 3, 0], "times_2_eval": [4, 2, 8, 2],
             },
             "add_il_element_one": {"x": [2, 1, 3, 2], "expected": [3, 2, 4, 3]},
+        },
+        "kat_nbtheory": {
+            "ref": "src/core/unittest/UnitTestNbTheory.cpp:165-186, 381-394",
+            "first_prime": [{"bits": 30, "m": 2048, "expected": 1073750017},
+                            {"bits": 49, "m": 4096, "expected": 562949953548289}],
+            "next_prime_chain": {"bits": 22, "m": 2048,
+                                 "expected": [4208641, 4263937, 4270081, 4274177, 4294657,
+                                              4300801, 4304897, 4319233, 4323329, 4360193]},
         },
         "kat_fast_expand_crt_basis": {
             "ref": "src/pke/unittest/utbfvrns/UnitTestBFVrnsCRTOperations.cpp:290-376",

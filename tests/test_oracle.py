@@ -219,3 +219,23 @@ def test_kat_common_elements(O):
     assert O.mul_scalar(vec(so["eval_x"]), [2], q).reshape(-1).tolist() == so["times_2_eval"]
     one = k["add_il_element_one"]
     assert O.add_scalar(vec(one["x"]), [1], q).reshape(-1).tolist() == one["expected"]
+
+
+def test_kat_nbtheory(O):
+    """UnitTestNbTheory.cpp:165-186 (FirstPrime) and 381-394 (NextPrime chain):
+    the prime search behind the moduli chains, in the oracle and in bench.py's
+    own product-side chain (FirstPrime then PreviousPrime, poly-benchmark-16k.cpp:89-96)."""
+    import bench
+
+    k = REF["kat_nbtheory"]
+    for c in k["first_prime"]:
+        assert O.first_prime(c["bits"], c["m"]) == c["expected"]
+    ch = k["next_prime_chain"]
+    q = O.first_prime(ch["bits"], ch["m"])
+    got = []
+    for _ in ch["expected"]:
+        q = O.next_prime(q, ch["m"])
+        got.append(q)
+    assert got == ch["expected"]
+    for log_n, towers in ((14, 8), (16, 16), (17, 4)):
+        assert bench.moduli_chain(log_n, towers) == O.moduli_chain(log_n, towers)
