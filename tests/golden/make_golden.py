@@ -7,10 +7,11 @@ Two kinds of fixture live here:
    native code, compiled during the survey, run on the inputs described
    there).  These pin the oracle:
      - UnitTestTransform.cpp:60-94  CRT_polynomial_mult KAT (q=113, m=8)
-     - UnitTestMubintvec.cpp:276-359 1-limb vector ModAdd/ModSub/ModMul KAT
+     - UnitTestMubintvec.cpp:276-359 1-limb and 402-484 2-limb (a 52-bit
+       modulus, one native word here) vector ModAdd/ModSub/ModMul KATs
      - UnitTestNTT.cpp:53-133 round-trip inputs
      - UnitTestPolyElements.cpp:265-305 SwitchModulus KAT, 500-523
-       AutomorphismTransform KAT (q=73, m=8)
+       AutomorphismTransform KAT and 535-571 transposition (q=73, m=8)
      - UnitTestCommonElements.cpp:240-320 common_binary_ops and 381-446
        common_arithmetic_ops_element (q=73, m=8): Plus / Minus / Times in
        evaluation form, SwitchFormat -> Times -> SwitchFormat, scalar ops;
@@ -62,6 +63,30 @@ def reference_fixtures():
             "modmul": [69404, 64196, 13039, 115321, 28519, 151998, 89117, 80908,
                        57386, 39364, 8355, 146135, 61336, 31598, 25961, 87680],
         },
+        "kat_mubintvec_2limb": {
+            "ref": "src/core/unittest/UnitTestMubintvec.cpp:402-484 (values < 2^52: one native word here)",
+            "q": 4057816419532801,
+            "a": [185225172798255, 98879665709163, 3497410031351258, 4012431933509255,
+                  1543020758028581, 135094568432141, 3976954337141739, 4030348521557120,
+                  175940803531155, 435236277692967, 3304652649070144, 2032520019613814,
+                  375749152798379, 3933203511673255, 2293434116159938, 1201413067178193],
+            "b": [698898215124963, 39832572186149, 1835473200214782, 1041547470449968,
+                  1076152419903743, 433588874877196, 2336100673132075, 2990190360138614,
+                  754647536064726, 702097990733190, 2102063768035483, 119786389165930,
+                  3976652902630043, 3238750424196678, 2978742255253796, 2124827461185795],
+            "modadd": [884123387923218, 138712237895312, 1275066812033239, 996162984426422,
+                       2619173177932324, 568683443309337, 2255238590741013, 2962722462162933,
+                       930588339595881, 1137334268426157, 1348899997572826, 2152306408779744,
+                       294585635895621, 3114137516337132, 1214359951880933, 3326240528363988],
+            "modsub": [3544143377206093, 59047093523014, 1661936831136476, 2970884463059287,
+                       466868338124838, 3759322113087746, 1640853664009664, 1040158161418506,
+                       3479109686999230, 3790954706492578, 1202588881034661, 1912733630447884,
+                       456912669701137, 694453087476577, 3372508280438943, 3134402025525199],
+            "modmul": [585473140075497, 3637571624495703, 1216097920193708, 1363577444007558,
+                       694070384788800, 2378590980295187, 903406520872185, 559510929662332,
+                       322863634303789, 1685429502680940, 1715852907773825, 2521152917532260,
+                       781959737898673, 2334258943108700, 2573793300043944, 1273980645866111],
+        },
         "roundtrip_ntt": {
             "ref": "src/core/unittest/UnitTestNTT.cpp:53-133",
             "m": 16,
@@ -81,6 +106,10 @@ def reference_fixtures():
             "ref": "src/core/unittest/UnitTestPolyElements.cpp:500-523",
             "q": 73, "m": 8, "root": 22, "format": "coefficient",
             "x": [56, 1, 37, 2], "k": 3, "expected": [56, 2, 36, 1],
+            # UnitTestPolyElements.cpp:535-571: Transpose() = AutomorphismTransform(m - 1)
+            # in evaluation form (poly-interface.h:443-450): SwitchFormat, Transpose, SwitchFormat
+            "transpose": {"ref": "src/core/unittest/UnitTestPolyElements.cpp:535-571",
+                          "x": [31, 21, 15, 34], "k": 7, "expected": [31, 39, 58, 52]},
         },
         "kat_common_elements": {
             "ref": "src/core/unittest/UnitTestCommonElements.cpp:240-320, 381-446, 457-483",

@@ -93,6 +93,29 @@ def test_kat_mubintvec(hip):
         assert host(c).tolist() == k["mod" + op], op
 
 
+@pytest.mark.parametrize("log_n,batch", [(4, 1), (16, 3)])
+def test_kat_mubintvec_2limb(hip, log_n, batch):
+    """UnitTestMubintvec.cpp:402-484 (a 52-bit modulus) through the element-wise
+    kernels, the 16-element vectors tiled to N = 2^log_n over `batch` entries."""
+    import torch
+
+    H, ctx = hip
+    k = REF["kat_mubintvec_2limb"]
+    q = k["q"]  # = 1 mod 2^20: an NTT modulus up to N = 2^19; root from the oracle rule
+    n = 1 << log_n
+    g = next(r for r in range(2, 1000) if pow(r, (q - 1) // 2, q) == q - 1)
+    psi = pow(g, (q - 1) // (2 * n), q)
+    plan = H.NTTPlan(ctx, log_n, [q], [psi])
+    reps = n // 16
+    tile = lambda v: np.tile(np.array(v, np.uint64), batch * reps).reshape(batch, 1, n)  # noqa: E731
+    a, b = dev(tile(k["a"])), dev(tile(k["b"]))
+    for op in ("add", "sub", "mul"):
+        c = torch.empty_like(a)
+        getattr(plan, "mod_" + op)(a.data_ptr(), b.data_ptr(), c.data_ptr(), batch, stream())
+        assert np.array_equal(host(c), tile(k["mod" + op])), op
+    plan.close()
+
+
 def test_kat_common_elements(hip):
     """UnitTestCommonElements.cpp (q = 73, N = 4) through the C ABI:
     common_binary_ops (240-320) -- evaluation-form Plus / Minus / Times and

@@ -101,6 +101,13 @@ def test_automorphism_reference_kat(hip):
     plan.automorphism(k["k"], True, x.data_ptr(), y.data_ptr(), 1, stream())
     plan.inverse(y.data_ptr(), 1, stream())
     assert host(y).reshape(-1).tolist() == k["expected"]
+    # UnitTestPolyElements.cpp:535-571: Transpose = AutomorphismTransform(m - 1), evaluation form
+    t = k["transpose"]
+    x = dev(np.array(t["x"], np.uint64).reshape(1, 1, 4))
+    plan.forward(x.data_ptr(), 1, stream())
+    plan.automorphism(t["k"], True, x.data_ptr(), y.data_ptr(), 1, stream())
+    plan.inverse(y.data_ptr(), 1, stream())
+    assert host(y).reshape(-1).tolist() == t["expected"]
 
 
 @pytest.mark.parametrize("log_n,towers,batch,b0", [(3, 3, 4, 0), (14, 2, 3, 5), (16, 2, 2, 1021)])

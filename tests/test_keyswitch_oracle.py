@@ -187,3 +187,8 @@ def test_automorphism_reference_kat():
     ev = O.ntt_fwd(x.reshape(1, 1, 4), tb).reshape(-1)
     back = O.ntt_inv(K.automorphism(ev, k["k"], True, k["q"]).reshape(1, 1, 4), tb).reshape(-1)
     assert back.tolist() == k["expected"]
+    # UnitTestPolyElements.cpp:535-571: Transpose = AutomorphismTransform(m - 1), evaluation form
+    t = k["transpose"]
+    ev = O.ntt_fwd(np.array(t["x"], np.uint64).reshape(1, 1, 4), tb).reshape(-1)
+    back = O.ntt_inv(K.automorphism(ev, t["k"], True, k["q"]).reshape(1, 1, 4), tb).reshape(-1)
+    assert back.tolist() == t["expected"]

@@ -29,6 +29,15 @@ def test_kat_mubintvec(O):
         assert O.eltwise(op, a, b, [k["q"]]).reshape(-1).tolist() == k["mod" + op]
 
 
+def test_kat_mubintvec_2limb(O):
+    """UnitTestMubintvec.cpp:402-484 basic_vector_vector_mod_math_2_limb (q < 2^52)."""
+    k = REF["kat_mubintvec_2limb"]
+    a = O.U(k["a"]).reshape(1, 1, -1)
+    b = O.U(k["b"]).reshape(1, 1, -1)
+    for op in ("add", "sub", "mul"):
+        assert O.eltwise(op, a, b, [k["q"]]).reshape(-1).tolist() == k["mod" + op]
+
+
 @pytest.mark.parametrize("bits,towers", [(22, 1), (28, 2)])
 def test_ntt_roundtrip_reference_inputs(O, bits, towers):
     """UnitTestNTT.cpp:53-133: SwitchFormat twice is the identity."""
