@@ -16,6 +16,8 @@ Two kinds of fixture live here:
        common_arithmetic_ops_element (q=73, m=8): Plus / Minus / Times in
        evaluation form, SwitchFormat -> Times -> SwitchFormat, scalar ops;
        457-483 AddILElementOne
+     - UnitTestDCRTElements.cpp:285-417 three-tower Plus / Minus / Times /
+       AddILElementOne in evaluation form
      - UnitTestNbTheory.cpp:165-186 FirstPrime KATs and 381-394 the NextPrime
        chain (the moduli generation behind every plan)
      - UnitTestBFVrnsCRTOperations.cpp:290-376 FastExpandCRTBasisPloverQ KAT
@@ -124,6 +126,12 @@ def reference_fixtures():
                 "eval_x": [2, 1, 4, 1], "minus_1_eval": [1, 0, 3, 0], "times_2_eval": [4, 2, 8, 2],
             },
             "add_il_element_one": {"x": [2, 1, 3, 2], "expected": [3, 2, 4, 3]},
+        },
+        "kat_dcrt_arithmetic": {
+            "ref": "src/core/unittest/UnitTestDCRTElements.cpp:285-417",
+            "m": 8, "q": [8353, 8369, 8513], "root": [8163, 6677, 156],
+            "a": [2, 4, 3, 2], "b": [2, 1, 2, 0],
+            "plus": [4, 5, 5, 2], "minus": [0, 3, 1, 2], "times": [4, 4, 6, 0], "add_one": [3, 5, 4, 3],
         },
         "kat_nbtheory": {
             "ref": "src/core/unittest/UnitTestNbTheory.cpp:165-186, 381-394",

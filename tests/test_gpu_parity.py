@@ -116,6 +116,26 @@ def test_kat_mubintvec_2limb(hip, log_n, batch):
     plan.close()
 
 
+def test_kat_dcrt_arithmetic(hip):
+    """UnitTestDCRTElements.cpp:285-417 (three towers 8353 / 8369 / 8513, N = 4,
+    evaluation form) through the C ABI: Plus, Minus, Times, AddILElementOne."""
+    import torch
+
+    H, ctx = hip
+    k = REF["kat_dcrt_arithmetic"]
+    plan = H.NTTPlan(ctx, 2, k["q"], k["root"])
+    rep = lambda v: np.stack([np.array(v, np.uint64)] * 3)[None]  # noqa: E731
+    a, b = dev(rep(k["a"])), dev(rep(k["b"]))
+    for op, key in (("add", "plus"), ("sub", "minus"), ("mul", "times")):
+        c = torch.empty_like(a)
+        getattr(plan, "mod_" + op)(a.data_ptr(), b.data_ptr(), c.data_ptr(), 1, stream())
+        assert np.array_equal(host(c), rep(k[key])), op
+    c = torch.empty_like(a)
+    plan.mod_add_scalar(a.data_ptr(), [1, 1, 1], c.data_ptr(), 1, stream())
+    assert np.array_equal(host(c), rep(k["add_one"]))
+    plan.close()
+
+
 def test_kat_common_elements(hip):
     """UnitTestCommonElements.cpp (q = 73, N = 4) through the C ABI:
     common_binary_ops (240-320) -- evaluation-form Plus / Minus / Times and

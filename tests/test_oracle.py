@@ -248,3 +248,16 @@ def test_kat_nbtheory(O):
     assert got == ch["expected"]
     for log_n, towers in ((14, 8), (16, 16), (17, 4)):
         assert bench.moduli_chain(log_n, towers) == O.moduli_chain(log_n, towers)
+
+
+def test_kat_dcrt_arithmetic(O):
+    """UnitTestDCRTElements.cpp:285-417: a three-tower DCRTPoly (moduli 8353,
+    8369, 8513) in evaluation form, the same small values in every tower:
+    Plus / Minus / Times / AddILElementOne, tower by tower."""
+    k = REF["kat_dcrt_arithmetic"]
+    q = k["q"]
+    rep = lambda v: np.stack([O.U(v)] * len(q))[None]  # noqa: E731
+    a, b = rep(k["a"]), rep(k["b"])
+    for op, key in (("add", "plus"), ("sub", "minus"), ("mul", "times")):
+        assert np.array_equal(O.eltwise(op, a, b, q), rep(k[key])), op
+    assert np.array_equal(O.add_scalar(a, [1, 1, 1], q), rep(k["add_one"]))
