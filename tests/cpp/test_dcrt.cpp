@@ -196,6 +196,124 @@ int main() {
                                          146135, 61336, 31598, 25961, 87680}),
                   "ModMul *=");
     });
+    // UnitTestMubintvec.cpp:402-484 ("2 limb": a 52-bit modulus, one native word here)
+    TEST("UTmubintvec.basic_vector_vector_mod_math_2_limb", [] {
+        auto P = params(32, {4057816419532801ull});
+        std::vector<uint64_t> a{185225172798255, 98879665709163, 3497410031351258, 4012431933509255,
+                                1543020758028581, 135094568432141, 3976954337141739, 4030348521557120,
+                                175940803531155, 435236277692967, 3304652649070144, 2032520019613814,
+                                375749152798379, 3933203511673255, 2293434116159938, 1201413067178193};
+        std::vector<uint64_t> b{698898215124963, 39832572186149, 1835473200214782, 1041547470449968,
+                                1076152419903743, 433588874877196, 2336100673132075, 2990190360138614,
+                                754647536064726, 702097990733190, 2102063768035483, 119786389165930,
+                                3976652902630043, 3238750424196678, 2978742255253796, 2124827461185795};
+        DCRTPolyHip A(P, Format::EVALUATION), B(P, Format::EVALUATION);
+        A.SetValues(a, Format::EVALUATION);
+        B.SetValues(b, Format::EVALUATION);
+        EXPECT_EQ((A + B).GetValues(),
+                  (std::vector<uint64_t>{884123387923218, 138712237895312, 1275066812033239, 996162984426422,
+                                         2619173177932324, 568683443309337, 2255238590741013, 2962722462162933,
+                                         930588339595881, 1137334268426157, 1348899997572826, 2152306408779744,
+                                         294585635895621, 3114137516337132, 1214359951880933, 3326240528363988}),
+                  "ModAdd");
+        EXPECT_EQ((A - B).GetValues(),
+                  (std::vector<uint64_t>{3544143377206093, 59047093523014, 1661936831136476, 2970884463059287,
+                                         466868338124838, 3759322113087746, 1640853664009664, 1040158161418506,
+                                         3479109686999230, 3790954706492578, 1202588881034661, 1912733630447884,
+                                         456912669701137, 694453087476577, 3372508280438943, 3134402025525199}),
+                  "ModSub");
+        EXPECT_EQ((A * B).GetValues(),
+                  (std::vector<uint64_t>{585473140075497, 3637571624495703, 1216097920193708, 1363577444007558,
+                                         694070384788800, 2378590980295187, 903406520872185, 559510929662332,
+                                         322863634303789, 1685429502680940, 1715852907773825, 2521152917532260,
+                                         781959737898673, 2334258943108700, 2573793300043944, 1273980645866111}),
+                  "ModMul");
+    });
+    // UnitTestCommonElements.cpp:240-320, 381-446, 457-483 (q = 73, m = 8)
+    TEST("UTCommonElements.binary_and_scalar_ops", [] {
+        auto P = params(8, {73});
+        DCRTPolyHip A(P, Format::EVALUATION), B(P, Format::EVALUATION);
+        A.SetValues({2, 1, 1, 1}, Format::EVALUATION);
+        B.SetValues({1, 0, 1, 1}, Format::EVALUATION);
+        EXPECT_EQ(A.Plus(B).GetValues(), (std::vector<uint64_t>{3, 1, 2, 2}), "Plus");
+        EXPECT_EQ(A.Minus(B).GetValues(), (std::vector<uint64_t>{1, 1, 0, 0}), "Minus");
+        EXPECT_EQ(A.Times(B).GetValues(), (std::vector<uint64_t>{2, 0, 1, 1}), "Times");
+        DCRTPolyHip a3(P, Format::COEFFICIENT), a4(P, Format::COEFFICIENT);
+        a3.SetValues({2, 1, 1, 1}, Format::COEFFICIENT);
+        a4.SetValues({1, 0, 1, 1}, Format::COEFFICIENT);
+        a3.SwitchFormat();
+        a4.SwitchFormat();
+        DCRTPolyHip a5 = a3.Times(a4);
+        a5.SwitchFormat();
+        EXPECT_EQ(a5.GetValues(), (std::vector<uint64_t>{0, 72, 2, 4}), "Times using SwitchFormat");
+        DCRTPolyHip c(P, Format::COEFFICIENT);
+        c.SetValues({1, 3, 4, 1}, Format::COEFFICIENT);
+        EXPECT_EQ(c.Plus(uint64_t(1)).GetValues(), (std::vector<uint64_t>{2, 3, 4, 1}), "Plus(1), coefficient form");
+        DCRTPolyHip e(P, Format::EVALUATION);
+        e.SetValues({2, 1, 4, 1}, Format::EVALUATION);
+        EXPECT_EQ(e.Minus(uint64_t(1)).GetValues(), (std::vector<uint64_t>{1, 0, 3, 0}), "Minus(1)");
+        EXPECT_EQ(e.Times(std::vector<uint64_t>{2}).GetValues(), (std::vector<uint64_t>{4, 2, 8, 2}), "Times(2)");
+        DCRTPolyHip o(P, Format::EVALUATION);
+        o.SetValues({2, 1, 3, 2}, Format::EVALUATION);
+        EXPECT_EQ(o.Plus(uint64_t(1)).GetValues(), (std::vector<uint64_t>{3, 2, 4, 3}), "AddILElementOne");
+    });
+    // UnitTestPolyElements.cpp:535-571: Transpose = AutomorphismTransform(m - 1) in evaluation form
+    TEST("UTPoly.transposition", [] {
+        auto P = params(8, {73});
+        DCRTPolyHip x(P, Format::COEFFICIENT);
+        x.SetValues({31, 21, 15, 34}, Format::COEFFICIENT);
+        x.SwitchFormat();
+        DCRTPolyHip t = x.AutomorphismTransform(7);
+        t.SwitchFormat();
+        EXPECT_EQ(t.GetValues(), (std::vector<uint64_t>{31, 39, 58, 52}), "transposition");
+    });
+    // UnitTestDCRTElements.cpp:285-417: three towers, evaluation form
+    TEST("UTDCRTPoly.DCRT_arithmetic_ops_element", [] {
+        auto P = params(8, {8353, 8369, 8513});
+        auto rep = [](std::vector<uint64_t> v) {
+            std::vector<uint64_t> out;
+            for (int t = 0; t < 3; t++) out.insert(out.end(), v.begin(), v.end());
+            return out;
+        };
+        DCRTPolyHip A(P, Format::EVALUATION), B(P, Format::EVALUATION);
+        A.SetValues(rep({2, 4, 3, 2}), Format::EVALUATION);
+        B.SetValues(rep({2, 1, 2, 0}), Format::EVALUATION);
+        EXPECT_EQ(A.Plus(B).GetValues(), rep({4, 5, 5, 2}), "Plus");
+        EXPECT_EQ(A.Minus(B).GetValues(), rep({0, 3, 1, 2}), "Minus");
+        EXPECT_EQ(A.Times(B).GetValues(), rep({4, 4, 6, 0}), "Times");
+        EXPECT_EQ(A.Plus(uint64_t(1)).GetValues(), rep({3, 5, 4, 3}), "AddILElementOne");
+    });
+    // UnitTestBFVrnsCRTOperations.cpp:290-376: FastExpandCRTBasisPloverQ's R_l
+    // towers are ApproxSwitchCRTBasis (dcrtpoly-impl.h:1419-1441) with
+    // c_i = q_i - [R QHat_i^-1]_{q_i} and q_i^-1 mod r_j
+    // (bfvrns-cryptoparameters.cpp:501-523)
+    TEST("UTBFVrnsCRT.FastExpandCRTBasisPloverQ_Rl", [] {
+        const std::vector<uint64_t> q{1152921504606846577ull, 1152921504606846097ull};
+        const std::vector<uint64_t> r{1152921504606845777ull, 1152921504606845473ull};
+        auto PQ = params(16, q), PR = params(16, r);
+        std::vector<uint64_t> hinv, hmod;
+        for (size_t i = 0; i < 2; i++) {
+            const uint64_t qhinv = powmod(prod_mod(q, i, q[i]), q[i] - 2, q[i]);
+            const uint64_t rl = mulmod(r[0] % q[i], r[1] % q[i], q[i]);
+            hinv.push_back((q[i] - mulmod(rl, qhinv, q[i])) % q[i]);
+            for (auto rj : r) hmod.push_back(powmod(q[i] % rj, rj - 2, rj));
+        }
+        BaseConverter conv(*PQ, *PR, hinv, hmod);
+        DCRTPolyHip x(PQ, Format::COEFFICIENT);
+        x.SetValues({242947838436205858ull, 458804958636264704ull, 813208723994158017ull, 738376275125875131ull,
+                     269337450701982501ull, 633721177525656427ull, 406635995163024073ull, 763204304316606329ull,
+                     1024863409567898083ull, 845721255474383902ull, 537504300724180111ull, 1018489837930110795ull,
+                     112800627588840746ull, 1119710169440476902ull, 77894506676832730ull, 34149187620514595ull},
+                    Format::COEFFICIENT);
+        EXPECT_EQ(conv.ApproxSwitchCRTBasis(x, PR).GetValues(),
+                  (std::vector<uint64_t>{955839852875274614ull, 186398073668078476ull, 710455872402389881ull,
+                                         1065981546244475424ull, 1049296073052489283ull, 578396240339812092ull,
+                                         26954876970280156ull, 1019223053257416912ull, 874592295621923164ull,
+                                         585167928946466637ull, 612704504638527027ull, 551633899923050545ull,
+                                         758002500979691774ull, 694035684451390662ull, 625796987487151016ull,
+                                         96319544173820807ull}),
+                  "R_l towers");
+    });
     // UnitTestDCRTElements.cpp:549-590 (property oracle: (a op b).Mod(q))
     TEST("UTDCRTPoly.DCRT_mod_ops_on_two_elements", [] {
         std::vector<uint64_t> q{first_prime(24, 16)};
