@@ -357,6 +357,29 @@ def test_kat_fast_expand_crt_basis(hip, log_n):
     assert np.array_equal(host(out), want)
 
 
+@pytest.mark.parametrize("log_n,sq,sp", [(5, 256, 256), (12, 200, 56), (12, 17, 256)])
+def test_base_conversion_size_limits(hip, O, log_n, sq, sp):
+    """ApproxSwitchCRTBasis at the C ABI's basis limits (256 source or target
+    towers, ofhe_hip_bconv_create) against the oracle; 257 is refused."""
+    import torch
+
+    H, ctx = hip
+    n = 1 << log_n
+    chain, _ = O.moduli_chain(log_n, sq + sp)
+    q, p = chain[:sq], chain[sq:]
+    pre = O.base_conv_precompute(q, p)
+    x = O.uniform_dcrt(2, sq, n, q, 41)
+    bc = H.BaseConverter(ctx, log_n, q, p, [int(v) for v in pre["qhinv"]], [int(v) for v in pre["qhmodp"]])
+    out = torch.zeros((2, sp, n), dtype=torch.int64, device="cuda")
+    bc.switch(dev(x).data_ptr(), out.data_ptr(), 2, stream())
+    got = host(out)
+    for bi in range(2):
+        assert np.array_equal(got[bi], O.approx_switch_crt_basis(x[bi], q, p, pre)), bi
+    bc.close()
+    with pytest.raises(H.MathError):
+        H.BaseConverter(ctx, log_n, chain[:1] * 257, p[:1], [1] * 257, [1] * 257)
+
+
 def test_base_conversion_config5_shape(hip, O):
     """N = 2^17 digit -> complement (16 -> 17 towers), vs the oracle."""
     import torch
