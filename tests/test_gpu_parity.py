@@ -357,6 +357,37 @@ def test_kat_fast_expand_crt_basis(hip, log_n):
     assert np.array_equal(host(out), want)
 
 
+@pytest.mark.parametrize("log_n,towers,batch", [(4, 4096, 1), (11, 700, 1), (13, 300, 2)])
+def test_plan_tower_limits(hip, O, log_n, towers, batch):
+    """Plans up to the C ABI's 4096 towers (ofhe_hip_plan_create): forward,
+    inverse and the fused pipeline against the oracle on every tower; 4097
+    is refused."""
+    import torch
+
+    H, ctx = hip
+    n = 1 << log_n
+    qs, rs = O.moduli_chain(log_n, towers)
+    plan = H.NTTPlan(ctx, log_n, qs, rs)
+    tb = O.Tables(n, qs, rs)
+    a = O.uniform_dcrt(batch, towers, n, qs, 51)
+    b = O.uniform_dcrt(batch, towers, n, qs, 52)
+    x = dev(a)
+    plan.forward(x.data_ptr(), batch, stream())
+    assert np.array_equal(host(x), O.ntt_fwd(a, tb))
+    x = dev(a)
+    plan.inverse(x.data_ptr(), batch, stream())
+    assert np.array_equal(host(x), O.ntt_inv(a, tb))
+    xa, xb = dev(a), dev(b)
+    c = torch.empty_like(xa)
+    plan.ntt_mul_intt(xa.data_ptr(), xb.data_ptr(), c.data_ptr(), batch, stream())
+    assert np.array_equal(host(c), O.ntt_mul_intt(a, b, tb))
+    plan.close()
+    if towers == 4096:
+        q2, r2 = O.moduli_chain(log_n, 4097)
+        with pytest.raises(H.MathError):
+            H.NTTPlan(ctx, log_n, q2, r2)
+
+
 @pytest.mark.parametrize("log_n,sq,sp", [(5, 256, 256), (12, 200, 56), (12, 17, 256)])
 def test_base_conversion_size_limits(hip, O, log_n, sq, sp):
     """ApproxSwitchCRTBasis at the C ABI's basis limits (256 source or target
