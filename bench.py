@@ -754,7 +754,11 @@ def bench_keyswitch(args, ctx, world, rank, dev, steps, warmup, with_stages=Fals
     allq, allr = moduli_chain(log_n, sq + sp_)
     q, rq, p, rp = allq[:sq], allr[:sq], allq[sq:], allr[sq:]
     B = args.ks_batch
-    ks = H.KeySwitch(ctx, log_n, q, rq, p, rp, dnum)
+    # BENCH_KS_SINGLE_STREAM=1: every digit on one stream (serial kernels, for
+    # per-kernel PMC passes, tools/pmc_ks.sh)
+    kso = H.KsOptions()
+    kso.single_stream = 1 if os.environ.get("BENCH_KS_SINGLE_STREAM") == "1" else 0
+    ks = H.KeySwitch(ctx, log_n, q, rq, p, rp, dnum, kso)
     _, beta = ks.digits(sq)
     pq = H.NTTPlan(ctx, log_n, q, rq)
     pqp = H.NTTPlan(ctx, log_n, q + p, rq + rp)

@@ -105,6 +105,25 @@ int ofhe_hip_trim(ofhe_ctx_t ctx, size_t keep_bytes);
  *      Tables are built on the host once and kept resident on the device. */
 int ofhe_hip_plan_create(ofhe_ctx_t ctx, uint32_t log_n, uint32_t towers, const uint64_t* q,
                          const uint64_t* psi, ofhe_plan_t* plan);
+/* Kernel choices of a plan, fixed at creation (ofhe_hip_plan_create_ex).  A
+ * zero-initialised struct (or NULL) is exactly ofhe_hip_plan_create's choice.
+ * Every setting gives the same canonical results; they let tests reach every
+ * kernel and A/B timings compare them in one process.  No reference
+ * counterpart (the reference has one CPU loop, transformnat-impl.h:300-354). */
+enum {
+    OFHE_SPLIT_AUTO = 0, /* log_n = 16: OFHE_SPLIT_8_8; other log_n > 12: OFHE_SPLIT_COLS  */
+    OFHE_SPLIT_COLS = 1, /* log_n - 12 column stages (k_cols) + a 12-stage block pass     */
+    OFHE_SPLIT_8_8 = 2,  /* log_n = 16 only: 8 column stages (k_tcols) + 8-stage block    */
+    OFHE_SPLIT_9_8 = 3,  /* log_n = 17 only: 9 column stages (k_tcols9) + 8-stage block   */
+    OFHE_SPLIT_8_9 = 4   /* log_n = 17 only: 8 column stages (k_tcols) + 9-stage block    */
+};
+typedef struct ofhe_plan_options {
+    uint32_t split;          /* OFHE_SPLIT_*; log_n <= 12 plans accept only AUTO          */
+    uint32_t generic_moduli; /* 1: the generic-modulus kernels even when every q is a
+                                special prime 2^L - d (the default picks the faster ones) */
+} ofhe_plan_options;
+int ofhe_hip_plan_create_ex(ofhe_ctx_t ctx, uint32_t log_n, uint32_t towers, const uint64_t* q,
+                            const uint64_t* psi, const ofhe_plan_options* options, ofhe_plan_t* plan);
 int ofhe_hip_plan_destroy(ofhe_plan_t plan);
 /* Performance knob for ofhe_hip_ntt_mul_intt at log_n > 12: process the batch
  * in chunks of `chunk_batch` entries (0 = whole batch in one pass) and, with
@@ -113,22 +132,6 @@ int ofhe_hip_plan_destroy(ofhe_plan_t plan);
  * setting; only speed changes.  Set it while no other thread launches with
  * the same plan: the launches read the setting without taking the plan's lock. */
 int ofhe_hip_plan_tune(ofhe_plan_t plan, uint32_t chunk_batch, uint32_t streams);
-/* Performance knob for ofhe_hip_ntt_mul_intt at log_n = 16 (the SwitchFormat ->
- * Times -> SwitchFormat chain of dcrtpoly-impl.h:2518-2524 / dcrtpoly.h:185-200):
- * persistent = 1 runs the three passes as one persistent launch whose XCDs
- * each drain a software-pipelined queue of (pass, tower) work items, lag =
- * steps between a tower's passes (0 = default); persistent = 0 restores the
- * three launches.  Fails with OFHE_ERR_STATE when the plan cannot run it
- * (log_n != 16, or the device's workgroup placement did not pass the plan's
- * one-time XCD probe).  Chunking (ofhe_hip_plan_tune) takes precedence.
- * Results are identical either way.  As for ofhe_hip_plan_tune, switch it
- * while no other thread launches with the same plan. */
-int ofhe_hip_plan_pipeline(ofhe_plan_t plan, int persistent, uint32_t lag);
-/* Whether the persistent pipeline is selected, and how many of its waits gave
- * up since the plan was created (0 unless an invariant broke; the outputs of
- * such a call are not to be trusted).  Synchronises the device.  No
- * reference counterpart (diagnostics of ofhe_hip_plan_pipeline). */
-int ofhe_hip_plan_pipeline_status(ofhe_plan_t plan, int* persistent, uint32_t* faults);
 /* Copy the plan's host-side tables out (debug / parity tests): any pointer
  * may be NULL.  tab*: [towers][N] in OpenFHE order (Table[rev(i)] = psi^i). */
 int ofhe_hip_plan_tables(ofhe_plan_t plan, uint64_t* tab, uint64_t* tab_pre, uint64_t* itab,
@@ -233,6 +236,22 @@ typedef struct ofhe_bconv_s* ofhe_bconv_t;
 int ofhe_hip_bconv_create(ofhe_ctx_t ctx, uint32_t log_n, uint32_t size_q, uint32_t size_p,
                           const uint64_t* q, const uint64_t* p, const uint64_t* qhat_inv_modq,
                           const uint64_t* qhat_modp, ofhe_bconv_t* bconv);
+/* Kernel choices of a converter (ofhe_hip_bconv_create_ex; zero = the default
+ * of ofhe_hip_bconv_create).  Same results for every setting. */
+enum {
+    OFHE_BCONV_KERNEL_AUTO = 0, /* matrix cores (<= 64 sources, N >= 32), else LIMB / WIDE */
+    OFHE_BCONV_KERNEL_LIMB = 1, /* 30-bit limb sums on the VALU (<= 16 sources)            */
+    OFHE_BCONV_KERNEL_WIDE = 2  /* 128-bit sums on the VALU, any number of sources         */
+};
+typedef struct ofhe_bconv_options {
+    uint32_t kernel;        /* OFHE_BCONV_KERNEL_*                                          */
+    uint32_t separate_cols; /* 1: in ofhe_hip_approx_mod_up / _down at N = 2^17, the
+                               conversion and the targets' forward column pass as two
+                               kernels instead of the fused k_bconv_cols                  */
+} ofhe_bconv_options;
+int ofhe_hip_bconv_create_ex(ofhe_ctx_t ctx, uint32_t log_n, uint32_t size_q, uint32_t size_p,
+                             const uint64_t* q, const uint64_t* p, const uint64_t* qhat_inv_modq,
+                             const uint64_t* qhat_modp, const ofhe_bconv_options* options, ofhe_bconv_t* bconv);
 int ofhe_hip_bconv_destroy(ofhe_bconv_t bconv);
 int ofhe_hip_approx_switch_crt_basis(ofhe_bconv_t bconv, const uint64_t* x, uint64_t* out,
                                      uint32_t batch, void* stream);
@@ -269,6 +288,18 @@ typedef struct ofhe_ks_s* ofhe_ks_t;
 int ofhe_hip_ks_create(ofhe_ctx_t ctx, uint32_t log_n, uint32_t size_q, const uint64_t* q,
                        const uint64_t* psi_q, uint32_t size_p, const uint64_t* p, const uint64_t* psi_p,
                        uint32_t num_part_q, ofhe_ks_t* ks);
+/* Engine choices (ofhe_hip_ks_create_ex; zero / NULL = ofhe_hip_ks_create's
+ * defaults).  Same results for every setting. */
+typedef struct ofhe_ks_options {
+    ofhe_plan_options plan;   /* the engine's Q|P plan                                       */
+    uint32_t separate_cols;   /* 1: base conversion and forward column pass as two kernels   */
+    uint32_t separate_icol;   /* 1: the digits' inverse column pass as its own kernel        */
+    uint32_t chunk;           /* ciphertexts per ModUp chunk (0 = the whole batch)           */
+    uint32_t single_stream;   /* 1: every digit on the caller's stream (no side streams)     */
+} ofhe_ks_options;
+int ofhe_hip_ks_create_ex(ofhe_ctx_t ctx, uint32_t log_n, uint32_t size_q, const uint64_t* q,
+                          const uint64_t* psi_q, uint32_t size_p, const uint64_t* p, const uint64_t* psi_p,
+                          uint32_t num_part_q, const ofhe_ks_options* options, ofhe_ks_t* ks);
 int ofhe_hip_ks_destroy(ofhe_ks_t ks);
 /* alpha (towers per digit) and beta (digits at level size_ql, capped at
  * num_part_q), keyswitch-hybrid.cpp:341-345. */

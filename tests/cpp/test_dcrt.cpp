@@ -16,12 +16,40 @@ using namespace ofhe;
 typedef unsigned __int128 u128;
 
 static int g_fail = 0, g_run = 0;
-#define EXPECT_EQ(a, b, msg)                                                                 \
-    do {                                                                                     \
-        if (!((a) == (b))) {                                                                 \
-            std::printf("  FAIL %s:%d %s\n", __FILE__, __LINE__, std::string(msg).c_str()); \
-            g_fail++;                                                                        \
-        }                                                                                    \
+// got / expected printers: scalars print their value, vectors their length and
+// the first differing index with both words (so a red record says whether the
+// device returned zeros, stale memory or wrong residues)
+template <class T>
+static std::string show(const T& v) {
+    return std::to_string(v);
+}
+static std::string show(bool v) { return v ? "true" : "false"; }
+template <class T, class U>
+static std::string diff(const T& got, const U& want) {
+    return "got " + show(got) + ", expected " + show(want);
+}
+static std::string diff(const std::vector<uint64_t>& got, const std::vector<uint64_t>& want) {
+    std::string s = "got " + std::to_string(got.size()) + " words, expected " + std::to_string(want.size());
+    size_t bad = 0, first = SIZE_MAX;
+    for (size_t i = 0; i < got.size() && i < want.size(); i++)
+        if (got[i] != want[i]) bad++, first = std::min(first, i);
+    if (first != SIZE_MAX)
+        s += "; " + std::to_string(bad) + " differ, first at " + std::to_string(first) + ": got " +
+             std::to_string(got[first]) + ", expected " + std::to_string(want[first]);
+    return s;
+}
+static std::string diff(const DCRTPolyHip& got, const DCRTPolyHip& want) {
+    return diff(got.GetValues(), want.GetValues());
+}
+#define EXPECT_EQ(a, b, msg)                                                                          \
+    do {                                                                                              \
+        const auto& got_ = (a);                                                                       \
+        const auto& want_ = (b);                                                                      \
+        if (!(got_ == want_)) {                                                                       \
+            std::printf("  FAIL %s:%d %s: %s\n", __FILE__, __LINE__, std::string(msg).c_str(),        \
+                        diff(got_, want_).c_str());                                                   \
+            g_fail++;                                                                                 \
+        }                                                                                             \
     } while (0)
 #define EXPECT_THROW(stmt, ex, msg)                                                               \
     do {                                                                                          \
@@ -122,19 +150,31 @@ static std::vector<uint64_t> signed_residues(const std::vector<int64_t>& c, cons
     return out;
 }
 
-static void TEST(const char* name, const std::function<void()>& f) {
+// Tests register here and main() runs them: all (default), those whose name
+// contains --filter's argument or is named by --only, --list prints the names (one pytest item
+// each, tests/test_cpp_host.py), --repeat runs the selection that many times
+// in one process (a soak of the adapter path: pool reuse, copies, plans).
+static std::vector<std::pair<std::string, std::function<void()>>>& registry() {
+    static std::vector<std::pair<std::string, std::function<void()>>> r;
+    return r;
+}
+static void TEST(const char* name, const std::function<void()>& f) { registry().emplace_back(name, f); }
+static void run_one(const std::string& name, const std::function<void()>& f) {
     int before = g_fail;
     g_run++;
     try {
         f();
     } catch (const std::exception& e) {
-        std::printf("  FAIL %s: exception %s\n", name, e.what());
+        std::printf("  FAIL %s: exception %s\n", name.c_str(), e.what());
         g_fail++;
     }
-    std::printf("[%s] %s\n", g_fail == before ? "  OK  " : " FAIL ", name);
+    std::printf("[%s] %s\n", g_fail == before ? "  OK  " : " FAIL ", name.c_str());
 }
 
-int main() {
+static int run_main(int argc, char** argv);
+int main(int argc, char** argv) { return run_main(argc, argv); }
+
+static void register_tests() {
     // UnitTestTransform.cpp:60-94
     TEST("UTTransform.CRT_polynomial_mult", [] {
         auto P = params(8, {113});
@@ -326,10 +366,23 @@ int main() {
         DCRTPolyHip A(P, Format::EVALUATION), B(P, Format::EVALUATION);
         A.SetValues(a, Format::EVALUATION);
         B.SetValues(b, Format::EVALUATION);
-        auto s = (A + B).GetValues(), p = (A * B).GetValues();
+        DCRTPolyHip S = A + B, M = A * B;
+        auto s = S.GetValues(), p = M.GetValues();
+        std::vector<uint64_t> ws(24), wp(24);
         for (size_t i = 0; i < 24; i++) {
-            EXPECT_EQ(s[i], (a[i] + b[i]) % q[i / 8], "sum index " + std::to_string(i));
-            EXPECT_EQ(p[i], (uint64_t)((u128)a[i] * b[i] % q[i / 8]), "prod index " + std::to_string(i));
+            ws[i] = (a[i] + b[i]) % q[i / 8];
+            wp[i] = (uint64_t)((u128)a[i] * b[i] % q[i / 8]);
+        }
+        EXPECT_EQ(s, ws, "sum");
+        EXPECT_EQ(p, wp, "prod");
+        if (s != ws || p != wp) {
+            // which stage lost the words: the operands on the device, the
+            // results, or the read-back (a second download of the same buffers)
+            EXPECT_EQ(A.GetValues(), a, "operand A on the device");
+            EXPECT_EQ(B.GetValues(), b, "operand B on the device");
+            EXPECT_EQ(S.GetValues(), ws, "sum, downloaded again");
+            EXPECT_EQ(M.GetValues(), wp, "prod, downloaded again");
+            EXPECT_EQ((A + B).GetValues(), ws, "sum, recomputed");
         }
     });
     // DCRTPoly SwitchFormat -> Times -> SwitchFormat vs the fused kernel, N = 2^14, 8 towers
@@ -701,6 +754,39 @@ int main() {
         EXPECT_THROW(DCRTParams(12, {17}, {3}), math_error, "non power of two order");
         EXPECT_THROW(DCRTParams(16, {first_prime(22, 16) + 2}, {3}), math_error, "bad modulus");
     });
+}
+
+static int run_main(int argc, char** argv) {
+    std::string filter, only;
+    int repeat = 1;
+    bool list = false;
+    for (int i = 1; i < argc; i++) {
+        const std::string a = argv[i];
+        if (a == "--filter" && i + 1 < argc) filter = argv[++i];
+        else if (a == "--only" && i + 1 < argc) only = argv[++i];
+        else if (a == "--repeat" && i + 1 < argc) repeat = std::max(1, std::atoi(argv[++i]));
+        else if (a == "--list") list = true;
+        else {
+            std::printf("usage: %s [--list] [--filter SUBSTR | --only NAME] [--repeat R]\n", argv[0]);
+            return 2;
+        }
+    }
+    register_tests();
+    if (list) {
+        for (auto& t : registry()) std::printf("%s\n", t.first.c_str());
+        return 0;
+    }
+    int selected = 0;
+    for (int r = 0; r < repeat; r++)
+        for (auto& t : registry())
+            if (only.empty() ? t.first.find(filter) != std::string::npos : t.first == only) {
+                run_one(t.first, t.second);
+                selected++;
+            }
+    if (!selected) {
+        std::printf("no test matches '%s'\n", only.empty() ? filter.c_str() : only.c_str());
+        return 2;
+    }
     std::printf("%d tests, %d failures\n", g_run, g_fail);
     return g_fail ? 1 : 0;
 }

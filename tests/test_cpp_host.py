@@ -2,21 +2,44 @@
 The suite mirrors UnitTestTransform / UnitTestNTT / UnitTestMubintvec /
 UnitTestDCRTElements through upmem--openfhe_amd/host/ofhe_dcrt.hpp."""
 import os
+import re
 import subprocess
 
 import pytest
 from conftest import ROOT
 
-pytestmark = pytest.mark.gpu
+gpu = pytest.mark.gpu
 
 
-def test_cpp_adapter_suite():
+def _suite_names():
+    """The sub-tests of tests/cpp/test_dcrt.cpp, read from its source (no
+    binary needed to collect): one pytest item each, so a red sub-test names
+    itself and does not hide the rest of the suite behind one item."""
+    src = open(os.path.join(ROOT, "tests", "cpp", "test_dcrt.cpp")).read()
+    return re.findall(r'^    TEST\("([^"]+)"', src, re.M)
+
+
+@pytest.fixture(scope="module")
+def cpp_bins():
     d = os.path.join(ROOT, "tests", "cpp")
     subprocess.run(["make", "-s", "-C", d], check=True)
-    r = subprocess.run([os.path.join(d, "test_dcrt_bin")], capture_output=True, text=True, timeout=300)
+    return d
+
+
+def test_cpp_suite_listing_matches_source():
+    """The registry the binary runs is the list collected here (CPU-side)."""
+    names = _suite_names()
+    assert len(names) == len(set(names)) >= 20
+
+
+@gpu
+@pytest.mark.parametrize("name", _suite_names())
+def test_cpp_adapter(cpp_bins, name):
+    r = subprocess.run([os.path.join(cpp_bins, "test_dcrt_bin"), "--only", name], capture_output=True, text=True,
+                       timeout=300)
     print(r.stdout)
     assert r.returncode == 0, r.stdout + r.stderr
-    assert " 0 failures" in r.stdout
+    assert "1 tests, 0 failures" in r.stdout, r.stdout
 
 
 def _read_chain(path):
@@ -31,6 +54,7 @@ def _read_chain(path):
     return out
 
 
+@gpu
 def test_cpp_device_resident_chain(tmp_path):
     """tests/cpp/chain.cpp strings SwitchFormat -> Times -> SwitchFormat ->
     scalar Plus/Minus -> ApproxModUp -> KeySwitchCore -> ApproxModDown together
@@ -72,6 +96,7 @@ def test_cpp_device_resident_chain(tmp_path):
     assert np.array_equal(D.reshape(B, sq, n), O.ntt_fwd(z2, tq)), "ApproxModDown(P * ApproxModUp(z2)) = z2"
 
 
+@gpu
 def test_cpp_openfhe_hooks():
     """The RUN_ON_HIP hook bodies (host/ofhe_openfhe_hooks.hpp) instantiated on a
     tower type with the reference's accessor names, checked against the oracle

@@ -159,6 +159,30 @@ def test_base_conversion_max_sums(hip, sq, reps, log_n):
     assert np.array_equal(host(out)[0], want)
 
 
+@pytest.mark.parametrize("sq,sp,log_n", [(3, 5, 5), (16, 48, 6), (12, 4, 12)])
+def test_base_conversion_kernel_options(hip, sq, sp, log_n):
+    """Every base-conversion kernel the converter options select (matrix
+    cores, 30-bit limbs, 128-bit sums) gives the oracle's ApproxSwitchCRTBasis
+    on the same inputs (extreme residues q - 1 in half the positions)."""
+    H, ctx = hip
+    import torch
+
+    n = 1 << log_n
+    q, rq, p, rp = _bases(log_n, sq, sp)
+    qhinv, qhmodp = K.switch_tables(q, p)
+    rng = np.random.default_rng(sq * 100 + sp)
+    x = _uniform(rng, 2, q, n)
+    x[:, :, ::2] = np.array(q, np.uint64)[None, :, None] - np.uint64(1)
+    want = K._switch_basis(x, q, p, qhinv, qhmodp)
+    dx = dev(x)
+    for kern in (H.BCONV_KERNEL_AUTO, H.BCONV_KERNEL_LIMB, H.BCONV_KERNEL_WIDE):
+        bc = H.BaseConverter(ctx, log_n, q, p, qhinv, [v for row in qhmodp for v in row], kernel=kern)
+        out = torch.zeros((2, sp, n), dtype=torch.int64, device="cuda")
+        bc.switch(dx.data_ptr(), out.data_ptr(), 2, stream())
+        assert np.array_equal(host(out), want), kern
+        bc.close()
+
+
 @pytest.mark.parametrize("sq", [3, 16])
 def test_base_conversion_special_primes(hip, sq):
     """Targets that are all of the form 2^L - d (k_bconv_mma's shift fold,
@@ -235,11 +259,11 @@ def test_keyswitch_inner_max_values(hip):
     assert np.array_equal(host(c0), r0) and np.array_equal(host(c1), r1)
 
 
-def _ks_case(H, ctx, log_n, sq, sp, dnum, generic=False):
+def _ks_case(H, ctx, log_n, sq, sp, dnum, generic=False, options=None):
     n = 1 << log_n
     q, rq, p, rp = (_generic_bases if generic else _bases)(log_n, sq, sp)
     kp = K.KeySwitchParams(n, q, rq, p, rp, dnum)
-    ks = H.KeySwitch(ctx, log_n, q, rq, p, rp, dnum)
+    ks = H.KeySwitch(ctx, log_n, q, rq, p, rp, dnum, options)
     return n, q, rq, p, rp, kp, ks
 
 
@@ -364,25 +388,27 @@ def test_keyswitch_bootstrap_shape(hip):
 
 @pytest.mark.parametrize("sq,sp,dnum,generic,B,cases,fused", [
     (48, 16, 3, False, 2, ((48, 0), (47, 0)), "1"),   # configs[4]; level 47: ModDown fused, ModUp not
-    (48, 16, 3, False, 1, ((48, 0),), "0"),           # the unfused kernels (OFHE_BCONV_COLS=0)
+    (48, 16, 3, False, 1, ((48, 0),), "0"),           # the unfused kernels (options.separate_cols)
     (12, 4, 3, False, 1, ((12, 0), (12, 65537), (11, 0)), "1"),
     (8, 4, 2, True, 2, ((8, 0), (7, 65537)), "1"),     # generic moduli: Mod<false>, no special-prime fold
     (10, 6, 4, False, 1, ((10, 0), (10, 3)), "1"),     # digits of 3 / 3 / 3 / 1 towers, 6 special towers
     (24, 12, 2, False, 1, ((24, 0),), "1"),            # 12-tower digits and P: the KS = 3 conversion kernels
 ])
 @pytest.mark.parametrize("icol", ["0", "1"])
-def test_keyswitch_bconv_cols(hip, monkeypatch, sq, sp, dnum, generic, B, cases, fused, icol):
+def test_keyswitch_bconv_cols(hip, sq, sp, dnum, generic, B, cases, fused, icol):
     """N = 2^17 KeySwitchCore with ApproxSwitchCRTBasis fused with the targets'
     forward column pass (k_bconv_cols, the default) in ModUp (full level) and
-    ModDown (t = 0), and with OFHE_BCONV_COLS=0, bit-exact against the oracle;
-    lower levels and t > 0 take the unfused kernels in the same call.  icol = 1
-    (OFHE_KS_ICOL) also moves the sources' INTT column pass into k_bconv_cols."""
+    ModDown (t = 0), and with options.separate_cols, bit-exact against the
+    oracle; lower levels and t > 0 take the unfused kernels in the same call.
+    icol = 1 (the default; options.separate_icol = 0) also moves the sources'
+    INTT column pass into k_bconv_cols."""
     H, ctx = hip
     import torch
 
-    monkeypatch.setenv("OFHE_BCONV_COLS", fused)
-    monkeypatch.setenv("OFHE_KS_ICOL", icol)
-    n, q, rq, p, rp, kp, ks = _ks_case(H, ctx, 17, sq, sp, dnum, generic)
+    opt = H.KsOptions()
+    opt.separate_cols = 0 if fused == "1" else 1
+    opt.separate_icol = 0 if icol == "1" else 1
+    n, q, rq, p, rp, kp, ks = _ks_case(H, ctx, 17, sq, sp, dnum, generic, opt)
     rng = np.random.default_rng(1700 + sq)
     kb = _uniform(rng, dnum, q + p, n)
     ka = _uniform(rng, dnum, q + p, n)

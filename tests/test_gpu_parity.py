@@ -476,9 +476,10 @@ def test_generic_moduli_vs_oracle(hip, O, log_n, towers, batch):
     assert np.array_equal(got["pipeline"], O.ntt_mul_intt(a, b, tb))
 
 
-def test_special_prime_switch_identical(hip, O, monkeypatch):
+def test_special_prime_switch_identical(hip, O):
     """Special-prime and generic kernels give identical results on the same
-    (special-form) moduli; OFHE_NO_SPQ forces the generic instantiation."""
+    (special-form) moduli; the plan option generic_moduli forces the generic
+    instantiation."""
     import torch
 
     H, ctx = hip
@@ -488,10 +489,8 @@ def test_special_prime_switch_identical(hip, O, monkeypatch):
     a = O.uniform_dcrt(B, T, n, qs, 5)
     b = O.uniform_dcrt(B, T, n, qs, 6)
     outs = []
-    for env in (None, "1"):
-        if env:
-            monkeypatch.setenv("OFHE_NO_SPQ", env)
-        plan = H.NTTPlan(ctx, log_n, qs, rs)
+    for generic in (False, True):
+        plan = H.NTTPlan(ctx, log_n, qs, rs, generic_moduli=generic)
         xa, xb = dev(a), dev(b)
         xc = torch.empty_like(xa)
         plan.ntt_mul_intt(xa.data_ptr(), xb.data_ptr(), xc.data_ptr(), B, stream())
@@ -500,11 +499,11 @@ def test_special_prime_switch_identical(hip, O, monkeypatch):
     assert np.array_equal(outs[0], O.ntt_mul_intt(a, b, O.Tables(n, qs, rs)))
 
 
-@pytest.mark.parametrize("split", ["OFHE_SPLIT9", "OFHE_SPLIT89"])
+@pytest.mark.parametrize("split", ["SPLIT_9_8", "SPLIT_8_9"])
 @pytest.mark.parametrize("edge", [False, True])
-def test_split9_n17_vs_oracle(hip, O, monkeypatch, edge, split):
-    """N = 2^17 under OFHE_SPLIT9 (k_tcols9: 9 column stages + the 8-stage
-    block pass) and OFHE_SPLIT89 (k_tcols' 8 column stages on 512 columns +
+def test_split9_n17_vs_oracle(hip, O, edge, split):
+    """N = 2^17 under OFHE_SPLIT_9_8 (k_tcols9: 9 column stages + the 8-stage
+    block pass) and OFHE_SPLIT_8_9 (k_tcols' 8 column stages on 512 columns +
     the 9-stage block pass) gives the oracle's forward, inverse and pipeline
     outputs; edge = all-(q-1) inputs (lazy-reduction corners of the split)."""
     import torch
@@ -519,8 +518,7 @@ def test_split9_n17_vs_oracle(hip, O, monkeypatch, edge, split):
     else:
         a = O.uniform_dcrt(B, T, n, qs, 17)
     b = O.uniform_dcrt(B, T, n, qs, 18)
-    monkeypatch.setenv(split, "1")
-    plan = H.NTTPlan(ctx, log_n, qs, rs)
+    plan = H.NTTPlan(ctx, log_n, qs, rs, split=getattr(H, split))
     xa, xb = dev(a), dev(b)
     xc = torch.empty_like(xa)
     plan.ntt_mul_intt(xa.data_ptr(), xb.data_ptr(), xc.data_ptr(), B, stream())
@@ -532,8 +530,8 @@ def test_split9_n17_vs_oracle(hip, O, monkeypatch, edge, split):
     assert np.array_equal(host(xc), O.ntt_mul_intt(a, b, tb))
 
 
-def test_split4_identical(hip, O, monkeypatch):
-    """N = 2^16 under OFHE_SPLIT4 (4 column stages + a 12-stage block pass, so
+def test_split4_identical(hip, O):
+    """N = 2^16 under OFHE_SPLIT_COLS (4 column stages + a 12-stage block pass, so
     the inverse block twist covers groups of 4096 instead of 256) gives the
     same canonical results as the default 8 | 8 split."""
     import torch
@@ -546,17 +544,15 @@ def test_split4_identical(hip, O, monkeypatch):
     a = O.uniform_dcrt(B, T, n, qs, 7)
     b = O.uniform_dcrt(B, T, n, qs, 8)
     want_pipe, want_inv = O.ntt_mul_intt(a, b, tb), O.ntt_inv(a, tb)
-    for env in (None, "1"):
-        if env:
-            monkeypatch.setenv("OFHE_SPLIT4", env)
-        plan = H.NTTPlan(ctx, log_n, qs, rs)
+    for split in (H.SPLIT_AUTO, H.SPLIT_COLS):
+        plan = H.NTTPlan(ctx, log_n, qs, rs, split=split)
         xa, xb = dev(a), dev(b)
         xc = torch.empty_like(xa)
         plan.ntt_mul_intt(xa.data_ptr(), xb.data_ptr(), xc.data_ptr(), B, stream())
         xi = dev(a)
         plan.inverse(xi.data_ptr(), B, stream())
-        assert np.array_equal(host(xc), want_pipe), env
-        assert np.array_equal(host(xi), want_inv), env
+        assert np.array_equal(host(xc), want_pipe), split
+        assert np.array_equal(host(xi), want_inv), split
 
 
 def test_stream_ordered_alloc_and_zero(hip):
@@ -579,87 +575,16 @@ def test_stream_ordered_alloc_and_zero(hip):
     assert not h[: n // 2].any() and np.array_equal(h[n // 2:], np.arange(n // 2, n))
 
 
-@pytest.mark.parametrize("batch,edge", [(1, False), (17, False), (150, False), (3, True)])
-def test_block_mma_vs_oracle(hip, O, monkeypatch, batch, edge):
-    """N = 2^16 fused pipeline with the matrix-core block pass (k_block_mma,
-    csrc/ntt_mma.hpp): batches of 1, 17 (one partial iteration of 16) and 150
-    (two workgroup chunks of 128, the second ragged) equal the oracle and the
-    butterfly block pass (k_block, the default); edge = all-(q-1) inputs.
-    k_block_mma is opt-in (OFHE_NTT_MMA=1; DESIGN.md, rejected variants)."""
-    import torch
-
-    H, ctx = hip
-    log_n, T = 16, 2
-    n = 1 << log_n
-    qs, rs = O.moduli_chain(log_n, T)
-    tb = O.Tables(n, qs, rs)
-    if edge:
-        a = np.broadcast_to(np.array(qs, np.uint64)[None, :, None] - np.uint64(1), (batch, T, n)).copy()
-        b = a.copy()
-    else:
-        a = O.uniform_dcrt(batch, T, n, qs, 500 + batch)
-        b = O.uniform_dcrt(batch, T, n, qs, 600 + batch)
-    outs = []
-    for env in ("1", "0"):
-        monkeypatch.setenv("OFHE_NTT_MMA", env)
-        plan = H.NTTPlan(ctx, log_n, qs, rs)
-        xa, xb = dev(a), dev(b)
-        xc = torch.empty_like(xa)
-        plan.ntt_mul_intt(xa.data_ptr(), xb.data_ptr(), xc.data_ptr(), batch, stream())
-        outs.append(host(xc))
-        plan.close()
-    assert np.array_equal(outs[0], outs[1])
-    sel = slice(None) if batch <= 17 else [0, 127, 128, batch - 1]
-    assert np.array_equal(outs[0][sel], O.ntt_mul_intt(a[sel], b[sel], tb))
-
-
-@pytest.mark.parametrize("T,batch,edge", [(2, 1, False), (3, 5, False), (16, 2, False), (2, 3, True)])
-def test_block_m16_vs_oracle(hip, O, monkeypatch, T, batch, edge):
-    """N = 2^16 fused pipeline with the four-round matrix-core block pass
-    (k_block_m16, csrc/ntt_m16.hpp: twist, shared-F rounds, explicit twiddles)
-    equals the oracle and the butterfly block pass bit for bit; edge =
-    all-(q-1) inputs.  Opt-in at plan creation (OFHE_BLOCK_M16=1)."""
-    import torch
-
-    H, ctx = hip
-    log_n = 16
-    n = 1 << log_n
-    qs, rs = O.moduli_chain(log_n, T)
-    tb = O.Tables(n, qs, rs)
-    if edge:
-        a = np.broadcast_to(np.array(qs, np.uint64)[None, :, None] - np.uint64(1), (batch, T, n)).copy()
-        b = a.copy()
-    else:
-        a = O.uniform_dcrt(batch, T, n, qs, 700 + batch)
-        b = O.uniform_dcrt(batch, T, n, qs, 800 + batch)
-    outs = []
-    for env in ("1", "0"):
-        monkeypatch.setenv("OFHE_BLOCK_M16", env)
-        plan = H.NTTPlan(ctx, log_n, qs, rs)
-        xa, xb = dev(a), dev(b)
-        xc = torch.empty_like(xa)
-        plan.ntt_mul_intt(xa.data_ptr(), xb.data_ptr(), xc.data_ptr(), batch, stream())
-        outs.append(host(xc))
-        plan.close()
-    assert np.array_equal(outs[1], O.ntt_mul_intt(a, b, tb))
-    bad = np.argwhere(outs[0] != outs[1])
-    assert bad.size == 0, (len(bad), bad[:5].tolist())
-
-
-@pytest.mark.parametrize("scratch", [False, True])
-def test_chunked_pipeline_matches(hip, O, scratch, monkeypatch):
+def test_chunked_pipeline_matches(hip, O):
     """ofhe_hip_plan_tune chunking (opt-in A/B settings): chunks of 3 and 4
-    polynomials (a ragged last chunk) on one and two streams, intermediates
-    through c or through the reused chunk scratch (OFHE_CHUNK_SCRATCH), out of
-    place and in place, against the oracle's pipeline."""
+    polynomials (a ragged last chunk) on one and two streams, out of place and
+    in place, against the oracle's pipeline."""
     import torch
 
     H, ctx = hip
     log_n, T, B = 16, 3, 7
     n = 1 << log_n
     qs, rs = O.moduli_chain(log_n, T)
-    if scratch:
-        monkeypatch.setenv("OFHE_CHUNK_SCRATCH", "1")
     plan = H.NTTPlan(ctx, log_n, qs, rs)
     a = O.uniform_dcrt(B, T, n, qs, 71)
     b = O.uniform_dcrt(B, T, n, qs, 72)

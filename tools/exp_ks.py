@@ -50,19 +50,21 @@ for p in paths:
             getattr(L, name).restype, getattr(L, name).argtypes = res, args
     ctx = vp()
     assert L.ofhe_hip_init(0, ctypes.byref(ctx)) == 0
-    # EXP_TOGGLE=VAR: a second engine per library built with VAR=1 (plan-creation
-    # switches such as OFHE_SPLIT4), timed in the same interleaved rounds
-    # (EXP_TOGGLE="VAR=v;VAR2" adds one engine per entry; a bare VAR means VAR=1)
+    # EXP_TOGGLE="field=v;field2=v": one more engine per entry, created with
+    # those ofhe_ks_options fields set (ofhe_hip.KsOptions: separate_cols,
+    # separate_icol, chunk, single_stream, plan.split, plan.generic_moduli),
+    # timed in the same interleaved rounds
     toggle = os.environ.get("EXP_TOGGLE")
     for tv in [None] + (toggle.split(";") if toggle else []):
-        if tv:
-            tk, _, tval = tv.partition("=")
-            os.environ[tk] = tval or "1"
+        opt = ofhe_hip.KsOptions()
+        for kv in filter(None, (tv or "").split(",")):
+            k, _, v = kv.partition("=")
+            obj, fld = (opt.plan, k[5:]) if k.startswith("plan.") else (opt, k)
+            setattr(obj, fld, int(v or "1"))
         ks = vp()
-        assert L.ofhe_hip_ks_create(ctx, log_n, sq, arr(allq[:sq]), arr(allr[:sq]), sp, arr(allq[sq:]),
-                                    arr(allr[sq:]), dnum, ctypes.byref(ks)) == 0, L.ofhe_hip_last_error()
-        if tv:
-            del os.environ[tk]
+        assert L.ofhe_hip_ks_create_ex(ctx, log_n, sq, arr(allq[:sq]), arr(allr[:sq]), sp, arr(allq[sq:]),
+                                       arr(allr[sq:]), dnum, ofhe_hip._opt_ptr(opt), ctypes.byref(ks)) == 0, \
+            L.ofhe_hip_last_error()
         libs.append((os.path.basename(p) + (f"+{tv}" if tv else ""), L, ks))
 s = torch.cuda.current_stream()
 spt = vp(s.cuda_stream)

@@ -26,7 +26,8 @@ n = 1 << log_n
 qs, rs = bench.moduli_chain(log_n, T)
 arr = lambda v: (ctypes.c_uint64 * len(v))(*v)  # noqa: E731
 libs = []
-# EXP_CONFIGS: ';'-separated plan-creation environments, e.g. ";OFHE_SPLIT4=1;OFHE_NO_SPQ=1"
+# EXP_CONFIGS: ';'-separated plan options (ofhe_hip.PlanOptions fields), e.g.
+# ";split=1;generic_moduli=1" -- one engine per entry and library
 configs = os.environ.get("EXP_CONFIGS", "").split(";")
 for p in paths:
     L = ctypes.CDLL(p)
@@ -37,14 +38,13 @@ for p in paths:
     ctx = vp()
     assert L.ofhe_hip_init(0, ctypes.byref(ctx)) == 0
     for cfg in configs:
-        saved = dict(os.environ)
+        opt = ofhe_hip.PlanOptions()
         for kv in filter(None, cfg.split(",")):
             k, v = kv.split("=")
-            os.environ[k] = v
+            setattr(opt, k, int(v))
         plan = vp()
-        assert L.ofhe_hip_plan_create(ctx, log_n, T, arr(qs), arr(rs), ctypes.byref(plan)) == 0, L.ofhe_hip_last_error()
-        os.environ.clear()
-        os.environ.update(saved)
+        assert L.ofhe_hip_plan_create_ex(ctx, log_n, T, arr(qs), arr(rs), ofhe_hip._opt_ptr(opt),
+                                         ctypes.byref(plan)) == 0, L.ofhe_hip_last_error()
         libs.append((os.path.basename(p) + ("[" + cfg + "]" if cfg else ""), L, plan))
 
 g = torch.Generator(device="cuda")

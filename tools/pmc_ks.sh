@@ -6,7 +6,7 @@ R="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 OUT="$R/gpurun_out/pmc_ks"
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
-export OFHE_KS_STREAMS=1
+export BENCH_KS_SINGLE_STREAM=1
 pass() {  # name, counters...
   local name="$1"; shift
   timeout -s KILL 240 rocprofv3 --pmc "$@" --kernel-trace --output-format csv -d "$OUT/$name" -o run \

@@ -25,8 +25,6 @@ plan = H.NTTPlan(ctx, log_n, qs, rs)
 if os.environ.get("PS_TUNE"):  # "chunk,streams" for the whole pipeline (ofhe_hip_plan_tune)
     cb, ns = (int(x) for x in os.environ["PS_TUNE"].split(","))
     plan.tune(cb, ns)
-if os.environ.get("PS_PIPE"):  # lag of the persistent one-launch pipeline (ofhe_hip_plan_pipeline)
-    plan.pipeline(True, int(os.environ["PS_PIPE"]))
 s = torch.cuda.current_stream()
 a = torch.empty((B, T, n), dtype=torch.int64, device="cuda")
 b = torch.empty_like(a)

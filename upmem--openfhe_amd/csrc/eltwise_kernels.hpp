@@ -213,6 +213,7 @@ struct BconvArgs {
     u32 mm_tpc;           // target tiles per block (blockIdx.y chunk) that fit the LDS budget
     u32 lazy_out;         // internal callers: outputs in [0, 4p) (a forward NTT follows)
     u32 mm_spq;           // k_bconv_mma: every target a special prime (bm_reduce's shift fold)
+    u32 kernel;           // OFHE_BCONV_KERNEL_* (host-side choice in bconv_run)
 };
 
 template <int PT>

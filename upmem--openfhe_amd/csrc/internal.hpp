@@ -158,14 +158,7 @@ struct ofhe_plan_s {
     // pipeline tuning (ofhe_hip_plan_tune): batch entries per chunk (0 = all)
     // and internal streams the chunks alternate over (1 = caller's stream).
     ofhe::u32 chunk_batch = 0, nstreams = 1;
-    bool chunk_scratch = false;  // chunk intermediates in a reused scratch (OFHE_CHUNK_SCRATCH, A/B)
-    // persistent pipeline (k_pipe, pipe_kernels.hpp; ofhe_hip_plan_pipeline):
-    // selected, lag, grid, and the one-time XCD probe (0 not run, 1 passed,
-    // -1 failed / not applicable); d_pipe_err counts given-up waits
-    bool pipe = false, pipe_static = false;
-    ofhe::u32 pipe_lag = 4, pipe_grid = 0, pipe_nq = 8, pipe_pieces = 1, pipe_hm = 1;
-    int pipe_state = 0;
-    ofhe::u32* d_pipe_err = nullptr;
+    ofhe_plan_options opts{};  // the creation options (ofhe_hip_plan_create_ex)
     bool spq = false;     // every modulus is 2^L - d with d < 2^32 (special-prime kernels)
     // column | block pass split for log_n > 12 (SPLIT_*, ofhe_hip.hip):
     //   SPLIT_COLS  k_cols (log_n - 12 stages) + k_block NR = 3
@@ -177,21 +170,11 @@ struct ofhe_plan_s {
     hipStream_t st[2] = {nullptr, nullptr};
     hipEvent_t ev_fork = nullptr, ev_join[2] = {nullptr, nullptr};
     std::mutex fork_mu;  // guards st / ev_* (plan_tune, the two-stream pipeline)
-    // k_block_mma (ntt_mma.hpp): F_i / V_i fragments per (tower, group) and the
-    // per-tower reduction constants, built on the first fused call
     // rescaling scalar tables (keyswitch.hip: DropLastElementAndScale /
     // ModReduce), uploaded once per distinct content into memory no launch
     // has read yet, kept until destroy
     std::mutex tab_mu;
     std::map<std::vector<ofhe::u64>, ofhe::u64*> tabs;
-    void* d_nm = nullptr;
-    int nm_state = 0;  // 0 not built, 1 ready, -1 not applicable
-    std::mutex nm_mu;
-    // k_block_m16 (ntt_m16.hpp): F / F' fragments, reduction constants and
-    // twist / twiddle tables per tower, built on the first fused call
-    void* d_m16 = nullptr;
-    int m16_state = 0;  // 0 not built, 1 ready, -1 not applicable
-    std::mutex m16_mu;
 };
 
 struct ofhe_bconv_s {
@@ -204,8 +187,6 @@ struct ofhe_bconv_s {
     // calls upload nothing and never synchronise
     std::mutex tab_mu;
     std::map<std::vector<ofhe::u64>, ofhe::u64*> tabs;
-    // k_bconv_cols in ofhe_hip_approx_mod_up / _down: OFHE_BCONV_COLS read when
-    // the converter is created (0: the separate conversion and column-pass
-    // kernels, for A/B runs), as the key-switch engines read it at ks_create
+    // k_bconv_cols in ofhe_hip_approx_mod_up / _down (options.separate_cols = 0)
     bool bcols = true;
 };

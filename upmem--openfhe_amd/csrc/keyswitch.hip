@@ -327,10 +327,10 @@ struct ofhe_ks_s {
     u32 log_n = 0, size_q = 0, size_p = 0, num_part_q = 0, alpha = 0;
     std::vector<u64> q, p;
     ofhe_plan_t plan = nullptr;  // towers q[0..size_q) then p[0..size_p)
-    hipStream_t side[KS_NSIDE] = {};  // fork streams (OFHE_KS_STREAMS=1: none)
-    u32 chunk = 0;                    // ciphertexts per ModUp chunk (OFHE_KS_CHUNK; 0: the whole batch)
-    bool bcols = true;                // k_bconv_cols in ModUp / ModDown (OFHE_BCONV_COLS=0: off)
-    bool icol = true;                 // ... with the INTT's column pass inside it (OFHE_KS_ICOL=0: off)
+    hipStream_t side[KS_NSIDE] = {};  // fork streams (options.single_stream: none)
+    u32 chunk = 0;                    // ciphertexts per ModUp chunk (options.chunk; 0: the whole batch)
+    bool bcols = true;                // k_bconv_cols in ModUp / ModDown (options.separate_cols: off)
+    bool icol = true;                 // ... with the INTT's column pass inside it (options.separate_icol: off)
     std::mutex mu;
     std::map<u32, KsLevel*> levels;
 };
@@ -348,7 +348,16 @@ static void level_free(KsLevel* L) {
 int ofhe_hip_ks_create(ofhe_ctx_t ctx, uint32_t log_n, uint32_t size_q, const uint64_t* q, const uint64_t* psi_q,
                        uint32_t size_p, const uint64_t* p, const uint64_t* psi_p, uint32_t num_part_q,
                        ofhe_ks_t* out) {
+    return ofhe_hip_ks_create_ex(ctx, log_n, size_q, q, psi_q, size_p, p, psi_p, num_part_q, nullptr, out);
+}
+
+int ofhe_hip_ks_create_ex(ofhe_ctx_t ctx, uint32_t log_n, uint32_t size_q, const uint64_t* q, const uint64_t* psi_q,
+                          uint32_t size_p, const uint64_t* p, const uint64_t* psi_p, uint32_t num_part_q,
+                          const ofhe_ks_options* options, ofhe_ks_t* out) {
     if (!ctx || !q || !psi_q || !p || !psi_p || !out) return fail(OFHE_ERR_ARG, "NULL argument");
+    const ofhe_ks_options opt = options ? *options : ofhe_ks_options{};
+    if (opt.separate_cols > 1 || opt.separate_icol > 1 || opt.single_stream > 1)
+        return fail(OFHE_ERR_ARG, "options.separate_cols / separate_icol / single_stream must be 0 or 1");
     if (size_q < 1 || size_p < 1 || size_q + size_p > 256) return fail(OFHE_ERR_ARG, "size_q + size_p must be in [2, 256]");
     if (num_part_q < 1 || num_part_q > size_q) return fail(OFHE_ERR_ARG, "num_part_q must be in [1, size_q]");
     const u32 alpha = (size_q + num_part_q - 1) / num_part_q;
@@ -363,7 +372,7 @@ int ofhe_hip_ks_create(ofhe_ctx_t ctx, uint32_t log_n, uint32_t size_q, const ui
     all.insert(all.end(), mp.begin(), mp.end());
     roots.insert(roots.end(), psi_p, psi_p + size_p);
     ofhe_plan_t plan = nullptr;
-    RCCHK(ofhe_hip_plan_create(ctx, log_n, size_q + size_p, all.data(), roots.data(), &plan));
+    RCCHK(ofhe_hip_plan_create_ex(ctx, log_n, size_q + size_p, all.data(), roots.data(), &opt.plan, &plan));
     ofhe_ks_s* k = new (std::nothrow) ofhe_ks_s();
     if (!k) {
         ofhe_hip_plan_destroy(plan);
@@ -378,14 +387,10 @@ int ofhe_hip_ks_create(ofhe_ctx_t ctx, uint32_t log_n, uint32_t size_q, const ui
     k->q = mq;
     k->p = mp;
     k->plan = plan;
-    const char* bcc = getenv("OFHE_BCONV_COLS");  // k_bconv_cols (default on; 0: separate kernels, A/B)
-    k->bcols = !(bcc && atoi(bcc) == 0);          // read per engine, so tests can switch it
-    const char* ic = getenv("OFHE_KS_ICOL");  // default on; 0: the INTT's own column pass (A/B)
-    k->icol = !(ic && atoi(ic) == 0);
-    const char* ck = getenv("OFHE_KS_CHUNK");
-    if (ck) k->chunk = (u32)atoi(ck);
-    const char* ns = getenv("OFHE_KS_STREAMS");
-    if (!(ns && atoi(ns) == 1)) {
+    k->bcols = !opt.separate_cols;
+    k->icol = !opt.separate_icol;
+    k->chunk = opt.chunk;
+    if (!opt.single_stream) {
         hipError_t e = hipSetDevice(ctx->device);
         for (int i = 0; i < KS_NSIDE && e == hipSuccess; i++)
             e = hipStreamCreateWithFlags(&k->side[i], hipStreamNonBlocking);

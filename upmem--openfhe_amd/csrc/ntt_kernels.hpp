@@ -122,7 +122,7 @@ __device__ __forceinline__ void st_s(u64* p, u64 v) {
 }
 // streaming (NT = true, as ld_s / st_s) or cached access, chosen per call site;
 // ld_m<LD_SC1> loads with sc1 (served by the XCD's L2, bypassing the CU's L1:
-// data another CU of the same XCD stored in this launch, k_pipe)
+// data another CU of the same XCD stored in the same launch)
 enum { LD_PLAIN = 0, LD_NT = 1, LD_SC1 = 2 };
 template <int LD>
 __device__ __forceinline__ u64 ld_m(const u64* p) {
@@ -613,7 +613,9 @@ __device__ __forceinline__ void wave_stage_out(const u64 (&v)[16], u64* lds, u32
 // tower pb = wid / G), on the caller's LDS (LDS_WORDS words).  IM: bit 0 =
 // the input is an intermediate another pass of the same launch wrote (cached
 // loads), bit 1 = the output is one (cached stores), bit 2 = load that input
-// with sc1 (L1 bypass, no acquire needed) -- k_pipe; 0 streams both.
+// with sc1 (L1 bypass, no acquire needed) -- for a pass fed by another pass
+// of the same launch (round 4's persistent pipeline, removed in round 5);
+// 0 streams both.
 template <int MODE, bool SPQ, int NR, int SK = 0, int IM = 0>
 __device__ __forceinline__ void block_body(const PlanArgs& P, const u64* src, u64* dst, const u64* __restrict__ bdat,
                                            u32 batch, u32 wid, u64* lds, u32 tid) {
@@ -850,9 +852,6 @@ constexpr u32 TCOLS_LDS_WORDS = 16 * 16 * TCOLS_W + 16 * 16;
 #define OFHE_TCOLS_HALF_WAVES 5
 #endif
 constexpr u32 TCOLS_LDS_INV_WORDS = OFHE_TCOLS_HALF ? 8 * 16 * TCOLS_W : TCOLS_LDS_WORDS;
-#ifndef OFHE_TCOLS_LOOP
-#define OFHE_TCOLS_LOOP 1  // tiles per workgroup (diagnostic variant builds only)
-#endif
 // The body of k_tcols for work item wid (column tile cb = wid % (S / W) of
 // polynomial tower pb = wid / (S / W)) on the caller's LDS (TCOLS_LDS_WORDS);
 // IM as block_body's.
@@ -981,20 +980,7 @@ __global__ __launch_bounds__(16 * TCOLS_W, (INV && OFHE_TCOLS_HALF) ? OFHE_TCOLS
     PlanArgs P, const u64* src, u64* dst, u32 batch, u32 nwg, SwSrc SWA) {
     OFHE_VGPR_FLOOR();
     __shared__ u64 lds[INV ? TCOLS_LDS_INV_WORDS : TCOLS_LDS_WORDS];
-#if OFHE_TCOLS_LOOP > 1
-    // diagnostic (persistent-loop cost): each workgroup runs OFHE_TCOLS_LOOP
-    // tiles back to back, the grid shrunk by that factor (N = 2^16 launches)
-    for (u32 k = 0; k < OFHE_TCOLS_LOOP; k++) {
-        u32 ti = threadIdx.x;
-        asm volatile("" : "+v"(ti));
-        const u32 it = blockIdx.x + k * gridDim.x;
-        if (it >= nwg) break;  // launch sites that still size the grid to nwg
-        if (k) __syncthreads();
-        tcols_body<INV, SPQ, SWS, LOGN>(P, src, dst, batch, xcd_remap(it, nwg), SWA, lds, ti);
-    }
-#else
     tcols_body<INV, SPQ, SWS, LOGN>(P, src, dst, batch, xcd_remap(blockIdx.x, nwg), SWA, lds, threadIdx.x);
-#endif
 }
 
 // ---------------------------------------------------------------------------

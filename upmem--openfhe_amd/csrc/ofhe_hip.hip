@@ -17,10 +17,7 @@
 #include <thread>
 
 #include "internal.hpp"
-#include "ntt_mma.hpp"
-#include "ntt_m16.hpp"
 #include "bconv_cols.hpp"
-#include "pipe_kernels.hpp"
 
 using namespace ofhe;
 
@@ -195,9 +192,38 @@ int ofhe_hip_sync(ofhe_ctx_t ctx, void* stream) {
 // ---------------------------------------------------------------------------
 int ofhe_hip_plan_create(ofhe_ctx_t ctx, uint32_t log_n, uint32_t towers, const uint64_t* q,
                          const uint64_t* psi, ofhe_plan_t* plan) {
+    return ofhe_hip_plan_create_ex(ctx, log_n, towers, q, psi, nullptr, plan);
+}
+
+int ofhe_hip_plan_create_ex(ofhe_ctx_t ctx, uint32_t log_n, uint32_t towers, const uint64_t* q,
+                            const uint64_t* psi, const ofhe_plan_options* options, ofhe_plan_t* plan) {
     if (!ctx || !q || !psi || !plan) return fail(OFHE_ERR_ARG, "NULL argument");
     if (log_n < 1 || log_n > 17) return fail(OFHE_ERR_ARG, "log_n must be in [1, 17]");
     if (towers < 1 || towers > 4096) return fail(OFHE_ERR_ARG, "towers must be in [1, 4096]");
+    const ofhe_plan_options opt = options ? *options : ofhe_plan_options{};
+    if (opt.generic_moduli > 1) return fail(OFHE_ERR_ARG, "options.generic_moduli must be 0 or 1");
+    // Pass split for log_n > 12 (DESIGN.md "Why not a 10 | 6 split" and the
+    // rejected-variant table): 8 | 8 at N = 2^16 (k_tcols + an 8-stage block
+    // pass), k_cols + the 12-stage block pass elsewhere; the other splits are
+    // selectable for tests and A/B timing.
+    int split = log_n == 16 ? SPLIT_T8 : SPLIT_COLS;
+    switch (opt.split) {
+        case OFHE_SPLIT_AUTO: break;
+        case OFHE_SPLIT_COLS:
+            if (log_n <= 12) return fail(OFHE_ERR_ARG, "options.split: log_n <= 12 plans have no column pass");
+            split = SPLIT_COLS;
+            break;
+        case OFHE_SPLIT_8_8:
+            if (log_n != 16) return fail(OFHE_ERR_ARG, "options.split OFHE_SPLIT_8_8 needs log_n = 16");
+            split = SPLIT_T8;
+            break;
+        case OFHE_SPLIT_9_8:
+        case OFHE_SPLIT_8_9:
+            if (log_n != 17) return fail(OFHE_ERR_ARG, "options.split OFHE_SPLIT_9_8 / 8_9 need log_n = 17");
+            split = opt.split == OFHE_SPLIT_9_8 ? SPLIT_T9 : SPLIT_T8B9;
+            break;
+        default: return fail(OFHE_ERR_ARG, "options.split is not an OFHE_SPLIT_* value");
+    }
     const u32 N = 1u << log_n;
     const u64 m = 2ull * N;
     for (u32 t = 0; t < towers; t++) {
@@ -231,15 +257,6 @@ int ofhe_hip_plan_create(ofhe_ctx_t ctx, uint32_t log_n, uint32_t towers, const 
     // DIT inverse (ntt_kernels.hpp): dtw[t + k] = psi^(-k N / t) for t = 1..N/2,
     // k < t; the block pass's output twist, and twist_r = twist * 2^64 mod q
     std::vector<u64> dtw(2 * TN), twist(2 * TN), twist_r(2 * TN);
-    // 8-stage block pass (k_block NR = 2) with an 8-stage column pass at
-    // N = 2^16 (k_tcols; OFHE_SPLIT4 restores k_cols + NR = 3).  At N = 2^17
-    // the 9 | 8 split (k_tcols9) is opt-in, OFHE_SPLIT9: measured 4 % slower in
-    // key switching than k_cols (5 stages) + NR = 3 (rejected variants)
-    // OFHE_SPLIT89 at N = 2^17: k_tcols' 8 stages + a 9-stage block pass
-    int split = SPLIT_COLS;
-    if (log_n == 16 && !getenv("OFHE_SPLIT4")) split = SPLIT_T8;
-    if (log_n == 17 && getenv("OFHE_SPLIT9")) split = SPLIT_T9;
-    if (log_n == 17 && getenv("OFHE_SPLIT89")) split = SPLIT_T8B9;
     // PreCompute (transformnat-impl.h:708-763), one host thread per tower group
     auto build = [&](u32 t) {
         const u64 qt = q[t], ps = psi[t], psinv = invmod(ps, qt);
@@ -338,17 +355,9 @@ int ofhe_hip_plan_create(ofhe_ctx_t ctx, uint32_t log_n, uint32_t towers, const 
     }
     p->spq = true;
     for (u32 t = 0; t < towers; t++) p->spq = p->spq && tc[t].spq_sh != 0;
-    if (getenv("OFHE_NO_SPQ")) p->spq = false;  // A/B switch for tests and timing
-    p->chunk_scratch = getenv("OFHE_CHUNK_SCRATCH") != nullptr;
+    if (opt.generic_moduli) p->spq = false;
     p->split = split;
-    {
-        // opt-in (OFHE_NTT_MMA=1): k_block_mma measured 1.7x slower than
-        // k_block at its 2 waves per SIMD (rejected variants)
-        const char* nm = getenv("OFHE_NTT_MMA");
-        if (!nm || atoi(nm) == 0) p->nm_state = -1;
-        const char* m16 = getenv("OFHE_BLOCK_M16");  // k_block_m16 (A/B against k_block)
-        if (!m16 || atoi(m16) == 0) p->m16_state = -1;
-    }
+    p->opts = opt;
     hipError_t e = hipSetDevice(ctx->device);
     if (e == hipSuccess) e = hipMalloc(&p->d_tc, sizeof(TowerConst) * towers);
     if (e == hipSuccess) e = hipMalloc(&p->d_tw, sizeof(u64) * 2 * TN);
@@ -408,94 +417,6 @@ int ofhe_hip_plan_tune(ofhe_plan_t p, uint32_t chunk_batch, uint32_t streams) {
     return OFHE_OK;
 }
 
-// One-time check that k_pipe's queues map one-to-one onto XCDs: a grid of
-// k_pipe's size records the XCD of every workgroup, and all of 0 .. nq - 1
-// must occur and nothing else (SPX mode).  Synchronises; runs on the first
-// ofhe_hip_plan_pipeline(persistent = 1) only.
-static int pipe_probe(ofhe_plan_t p) {
-    int occ = 0, ncu = 0;
-    HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(
-        &occ, p->spq ? (const void*)k_pipe<true, 1> : (const void*)k_pipe<false, 1>, 256, 0));
-    HIPCHK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, p->ctx->device));
-    if (occ < 1 || ncu < 1) return fail(OFHE_ERR_STATE, "persistent pipeline: kernel does not fit a CU");
-    const u32 grid = (u32)occ * (u32)ncu;
-    u32* d = nullptr;
-    HIPCHK(hipMalloc(&d, sizeof(u32) * grid));
-    hipLaunchKernelGGL(k_pipe_probe, dim3(grid), dim3(256), 0, nullptr, d);
-    std::vector<u32> x(grid);
-    hipError_t e = hipGetLastError();
-    if (e == hipSuccess) e = hipMemcpy(x.data(), d, sizeof(u32) * grid, hipMemcpyDeviceToHost);
-    (void)hipFree(d);
-    if (e != hipSuccess) return fail(OFHE_ERR_HIP, std::string("persistent pipeline probe: ") + hipGetErrorString(e));
-    u32 seen = 0;
-    bool ok = true;
-    for (u32 v : x) {
-        if (v >= p->pipe_nq) ok = false;
-        else seen |= 1u << v;
-    }
-    if (!ok || seen != (1u << p->pipe_nq) - 1) {
-        p->pipe_state = -1;
-        return fail(OFHE_ERR_STATE, "persistent pipeline: workgroups do not map onto 8 XCDs (not SPX mode?)");
-    }
-    HIPCHK(hipMalloc(&p->d_pipe_err, sizeof(u32)));
-    HIPCHK(hipMemset(p->d_pipe_err, 0, sizeof(u32)));
-    HIPCHK(hipDeviceSynchronize());
-    p->pipe_grid = grid;
-    p->pipe_state = 1;
-    return OFHE_OK;
-}
-
-int ofhe_hip_plan_pipeline(ofhe_plan_t p, int persistent, uint32_t lag) {
-    if (!p || !p->ctx) return fail(OFHE_ERR_STATE, "plan is NULL or destroyed");
-    if (lag > (1u << 20)) return fail(OFHE_ERR_ARG, "lag must be <= 2^20");
-    HIPCHK(hipSetDevice(p->ctx->device));
-    std::lock_guard<std::mutex> lk(p->fork_mu);
-    if (!persistent) {
-        p->pipe = false;
-        return OFHE_OK;
-    }
-    if (p->log_n != 16 || p->split != SPLIT_T8)
-        return fail(OFHE_ERR_STATE, "persistent pipeline: log_n = 16 plans (8 | 8 pass split) only");
-    if (p->pipe_state == 0) RCCHK(pipe_probe(p));
-    if (p->pipe_state != 1) return fail(OFHE_ERR_STATE, "persistent pipeline: the XCD probe failed on this device");
-    p->pipe_lag = lag ? lag : 4;
-    // A/B knobs: hand-off mode (k_pipe HM), pieces per work item, static item assignment
-    p->pipe_hm = getenv("OFHE_PIPE_HM") ? (u32)atoi(getenv("OFHE_PIPE_HM")) & 3 : 1;
-    {
-        const char* e = getenv("OFHE_PIPE_PIECES");
-        const u32 v = e ? (u32)atoi(e) : 1;
-        p->pipe_pieces = (v == 2 || v == 4 || v == 8 || v == 16) ? v : 1;
-        p->pipe_static = getenv("OFHE_PIPE_STATIC") && atoi(getenv("OFHE_PIPE_STATIC")) != 0;
-    }
-    {
-        // OFHE_PIPE_WGS: workgroups per CU (A/B knob: fewer in flight per XCD
-        // means fewer towers' intermediates live in its L2); default: all fit
-        int occ = 0, ncu = 0;
-        HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(
-            &occ, p->spq ? (const void*)k_pipe<true, 1> : (const void*)k_pipe<false, 1>, 256, 0));
-        HIPCHK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, p->ctx->device));
-        const char* w = getenv("OFHE_PIPE_WGS");
-        if (w && atoi(w) > 0 && atoi(w) < occ) occ = atoi(w);
-        p->pipe_grid = (u32)occ * (u32)ncu;
-    }
-    p->pipe = true;
-    return OFHE_OK;
-}
-
-int ofhe_hip_plan_pipeline_status(ofhe_plan_t p, int* persistent, uint32_t* faults) {
-    if (!p || !p->ctx) return fail(OFHE_ERR_STATE, "plan is NULL or destroyed");
-    if (persistent) *persistent = p->pipe ? 1 : 0;
-    if (faults) {
-        *faults = 0;
-        if (p->d_pipe_err) {
-            HIPCHK(hipSetDevice(p->ctx->device));
-            HIPCHK(hipDeviceSynchronize());
-            HIPCHK(hipMemcpy(faults, p->d_pipe_err, sizeof(u32), hipMemcpyDeviceToHost));
-        }
-    }
-    return OFHE_OK;
-}
-
 int ofhe_hip_plan_destroy(ofhe_plan_t p) {
     if (!p) return fail(OFHE_ERR_ARG, "plan is NULL");
     if (p->ctx) (void)hipSetDevice(p->ctx->device);
@@ -512,9 +433,6 @@ int ofhe_hip_plan_destroy(ofhe_plan_t p) {
     (void)hipFree(p->d_dtw);
     (void)hipFree(p->d_twist);
     (void)hipFree(p->d_twist_r);
-    (void)hipFree(p->d_nm);
-    (void)hipFree(p->d_m16);
-    (void)hipFree(p->d_pipe_err);
     for (auto& kv : p->tabs) (void)hipFree(kv.second);
     delete p;
     return OFHE_OK;
@@ -664,7 +582,7 @@ static void launch_tcols(const PlanArgs& a, bool spq, int split, bool inv, const
     }
     const u32 nwg = batch * a.towers * (256 / TCOLS_W);
 #define LT(I, SP)                                                                                 \
-    hipLaunchKernelGGL((k_tcols<I, SP>), dim3(nwg / OFHE_TCOLS_LOOP), dim3(16 * TCOLS_W), 0, s, a, src, dst, batch, nwg, \
+    hipLaunchKernelGGL((k_tcols<I, SP>), dim3(nwg), dim3(16 * TCOLS_W), 0, s, a, src, dst, batch, nwg, \
                        SwSrc{nullptr, 0, 0, nullptr, 1, 0})
     if (inv) {
         if (spq) LT(true, true); else LT(true, false);
@@ -848,293 +766,6 @@ int ofhe_hip_ntt_inv_range(ofhe_plan_t p, uint32_t t0, uint32_t count, const uin
     return plan_ntt_range(p, true, t0, count, src, dst, src_stride, dst_stride, batch, pick(stream));
 }
 
-// ---------------------------------------------------------------------------
-// k_block_mma (ntt_mma.hpp): per tower t and group i the two 16 x 16 maps of
-// the block pass that do not depend on the column, as A-operand fragments of
-// v_mfma_i32_32x32x32_i8 in k_bconv_mma's layout (bconv_mma_table):
-//   F_i  forward CT stages m = 256 .. 2048 on elements i 256 + 16 j (column 0;
-//        every column has the same map), Table[m + e / (2t)];
-//   V_i  GS stages t = 16 .. 128, TableI[m + e / (2t)], times N^-1 2^64 (the
-//        2^64 cancels the Montgomery Hadamard's 2^-64).
-// Opt-in (OFHE_NTT_MMA=1 at plan creation): built on the first fused call of
-// a special-prime N = 2^16 plan (8 MiB per tower); never for other plans or a
-// modulus outside bm_reduce<SPQ>'s range.
-// ---------------------------------------------------------------------------
-// A-operand fragments of v_mfma_i32_32x32x32_i8 for a 16 x 16 map A[out][in]
-// mod q in k_bconv_mma's layout (bconv_mma.hpp): fragment (mt, s), lane l =
-// rr + 32 kh holds row rr of M-tile mt -- output k = 4 mt + 2 dh + (reg >> 3),
-// constant digit reg & 7, with dh = (rr >> 2) & 1, reg = (rr & 3) + 4 (rr >> 3)
-// -- over the K labels (input 4 s + 2 kh + (e >> 3), data digit e & 7): byte e
-// = signed digit of 2^(8 a) A[k][j] mod q.  16 KiB.
-static void frag16(const u64 (*A)[16], u64 q, unsigned char* dst) {
-    u64 pw[8];
-    for (u32 a = 0; a < 8; a++) pw[a] = (u64)(((u128)1 << (8 * a)) % q);
-    for (u32 mt = 0; mt < 4; mt++)
-        for (u32 s = 0; s < 4; s++)
-            for (u32 l = 0; l < 64; l++) {
-                const u32 rr = l & 31, kh = l >> 5;
-                const u32 dh = (rr >> 2) & 1, reg = (rr & 3) + 4 * (rr >> 3);
-                const u32 k = 4 * mt + 2 * dh + (reg >> 3), bd = reg & 7;
-                for (u32 e = 0; e < 16; e++) {
-                    const u32 j = 4 * s + 2 * kh + (e >> 3), a = e & 7;
-                    const u64 z = mulmod(pw[a], A[k][j], q) + DIGIT_BIAS;
-                    dst[(((size_t)mt * 4 + s) * 64 + l) * 16 + e] = (unsigned char)(((z >> (8 * bd)) & 0xFF) ^ 0x80);
-                }
-            }
-}
-
-// bm_reduce<.., SPQ> constants of q, and whether q is in its range
-static bool bm_red_spq(u64 q, BmRed& R) {
-    const unsigned L = msb64(q);
-    const u64 d = (1ull << L) - q;
-    if (!(L >= 33 && d < (1ull << 32) && (((u128)1 << (81 - L)) + 1) * d + ((u128)1 << 49) + 2 * (u128)d < ((u128)1 << L)))
-        return false;
-    R = BmRed{};
-    R.p = q;
-    R.np = 0 - q;
-    const u128 k = (((u128)1 << 80) + q - 1) / q;
-    const u128 bias = k * q;
-    R.bhi = (u64)(bias >> 32) - (1ull << 16);
-    R.blo = (u64)(bias & 0xFFFFFFFFull) + (1ull << 48);
-    R.p2 = 2 * q;
-    R.r60 = (1ull << L) - q;
-    R.r60p = (u64)(L - 32) | ((u64)((1u << (L - 32)) - 1) << 32);
-    return true;
-}
-
-#ifndef OFHE_NM_CHUNK
-#define OFHE_NM_CHUNK 128  // polynomials per workgroup (the batch loop of one group)
-#endif
-static bool nm_ready(ofhe_plan_t p) {
-    std::lock_guard<std::mutex> lk(p->nm_mu);
-    if (p->nm_state) return p->nm_state > 0;
-    p->nm_state = -1;
-    if (p->log_n != 16 || !p->spq || !p->split) return false;
-    const u32 T = p->towers, N = 1u << 16;
-    for (u32 t = 0; t < T; t++) {
-        BmRed R;
-        if (!bm_red_spq(p->q[t], R)) return false;
-    }
-    const size_t per_group = 2 * (size_t)NM_FRAG * 16;  // bytes
-    const size_t fbytes = (size_t)T * 256 * per_group;
-    std::vector<unsigned char> tab(fbytes + (size_t)T * sizeof(BmRed));
-    BmRed* red = reinterpret_cast<BmRed*>(tab.data() + fbytes);
-    auto build = [&](u32 t) {
-        const u64 q = p->q[t];
-        const u64* Tb = &p->tab[(size_t)t * N];
-        const u64* TI = &p->itab[(size_t)t * N];
-        const u64 scale = mulmod(p->ninv[t], (u64)(((u128)1 << 64) % q), q);
-        for (u32 i = 0; i < 256; i++) {
-            u64 F[16][16], V[16][16];  // [k][j]
-            for (u32 j0 = 0; j0 < 16; j0++) {
-                u64 v[16] = {}, x[16] = {};
-                v[j0] = 1;
-                x[j0] = 1;
-                for (u32 m = 256; m <= 2048; m <<= 1) {
-                    const u32 tt = N / (2 * m), tj = tt / 16;
-                    for (u32 j = 0; j < 16; j++) {
-                        if (j & tj) continue;
-                        const u32 e = i * 256 + 16 * j;
-                        const u64 w = Tb[m + e / (2 * tt)];
-                        const u64 a = v[j], b = mulmod(v[j + tj], w, q);
-                        v[j] = a + b >= q ? a + b - q : a + b;
-                        v[j + tj] = a >= b ? a - b : a + q - b;
-                    }
-                }
-                for (u32 tt = 16; tt <= 128; tt <<= 1) {
-                    const u32 m = N / (2 * tt), tj = tt / 16;
-                    for (u32 j = 0; j < 16; j++) {
-                        if (j & tj) continue;
-                        const u32 e = i * 256 + 16 * j;
-                        const u64 w = TI[m + e / (2 * tt)];
-                        const u64 a = x[j], b = x[j + tj];
-                        x[j] = a + b >= q ? a + b - q : a + b;
-                        x[j + tj] = mulmod(a >= b ? a - b : a + q - b, w, q);
-                    }
-                }
-                for (u32 k = 0; k < 16; k++) {
-                    F[k][j0] = v[k];
-                    V[k][j0] = mulmod(x[k], scale, q);
-                }
-            }
-            for (u32 mat = 0; mat < 2; mat++)
-                frag16(mat ? V : F, q, tab.data() + ((size_t)t * 256 + i) * per_group + (size_t)mat * NM_FRAG * 16);
-        }
-        (void)bm_red_spq(q, red[t]);
-    };
-    {
-        unsigned nth = std::thread::hardware_concurrency();
-        if (nth < 1) nth = 1;
-        if (nth > T) nth = T;
-        if (nth > 16) nth = 16;
-        std::vector<std::thread> th;
-        for (unsigned w = 0; w < nth; w++)
-            th.emplace_back([&, w] {
-                for (u32 t = w; t < T; t += nth) build(t);
-            });
-        for (auto& x : th) x.join();
-    }
-    void* d = nullptr;
-    if (hipMalloc(&d, tab.size()) != hipSuccess) return false;
-    if (upload_blocking(d, tab.data(), tab.size()) != hipSuccess) {
-        (void)hipFree(d);
-        return false;
-    }
-    p->d_nm = d;
-    p->nm_state = 1;
-    return true;
-}
-
-// k_block_m16 (ntt_m16.hpp) tables of an N = 2^16 special-prime plan, per
-// tower: F[r][j] = w16^(j rev4(r)) and F'[j][r] = w16^(-j rev4(r)) as
-// fragments (w16 = psi^(2N/16)), bm_reduce constants, the forward twist
-// theta_G^j = psi^((2 rev8(G) + 1) j) at element 256 G + j, and the twiddles
-// w256^(+-j0 rev4(r')) at [r'][j0] (w256 = psi^(2N/256)).  Opt-in with
-// OFHE_BLOCK_M16=1 at plan creation (A/B against k_block).
-static bool m16_ready(ofhe_plan_t p) {
-    std::lock_guard<std::mutex> lk(p->m16_mu);
-    if (p->m16_state) return p->m16_state > 0;
-    p->m16_state = -1;
-    if (p->log_n != 16 || !p->spq || !p->split) return false;
-    const u32 T = p->towers, N = 1u << 16;
-    for (u32 t = 0; t < T; t++) {
-        BmRed R;
-        if (!bm_red_spq(p->q[t], R)) return false;
-    }
-    const size_t fbytes = (size_t)T * 2 * 1024 * 16, rbytes = (size_t)T * sizeof(BmRed);
-    const size_t twords = (size_t)T * N * 2, wwords = (size_t)T * 1024;
-    std::vector<unsigned char> tab(fbytes + rbytes + (twords + wwords) * 8);
-    BmRed* red = reinterpret_cast<BmRed*>(tab.data() + fbytes);
-    u64* twf = reinterpret_cast<u64*>(tab.data() + fbytes + rbytes);
-    u64* w16 = twf + twords;
-    auto build = [&](u32 t) {
-        const u64 q = p->q[t], psi = p->psi[t];
-        const u64 w256 = powmod(psi, 2 * N / 256, q), w16r = powmod(w256, 16, q), w256i = invmod(w256, q);
-        u64 F[16][16], Fi[16][16];
-        for (u32 r = 0; r < 16; r++)
-            for (u32 j = 0; j < 16; j++) {
-                F[r][j] = powmod(w16r, (u64)j * bitrev(r, 4), q);
-                Fi[j][r] = powmod(w16r, (16 - ((u64)j * bitrev(r, 4)) % 16) % 16, q);
-            }
-        frag16(F, q, tab.data() + (size_t)t * 2 * 1024 * 16);
-        frag16(Fi, q, tab.data() + (size_t)t * 2 * 1024 * 16 + 1024 * 16);
-        (void)bm_red_spq(q, red[t]);
-        u64* tf = twf + (size_t)t * N * 2;
-        for (u32 G = 0; G < 256; G++) {
-            const u64 th = powmod(psi, 2 * (u64)bitrev(G, 8) + 1, q);
-            u64 f = 1;
-            for (u32 j = 0; j < 256; j++) {
-                tf[2 * (G * 256 + j)] = f;
-                tf[2 * (G * 256 + j) + 1] = shoup_pre(f, q);
-                f = mulmod(f, th, q);
-            }
-        }
-        u64* wf = w16 + (size_t)t * 1024;
-        for (u32 r1 = 0; r1 < 16; r1++)
-            for (u32 j0 = 0; j0 < 16; j0++) {
-                const u64 e = (u64)j0 * bitrev(r1, 4);
-                const u64 x = powmod(w256, e, q), y = powmod(w256i, e, q);
-                wf[2 * (r1 * 16 + j0)] = x;
-                wf[2 * (r1 * 16 + j0) + 1] = shoup_pre(x, q);
-                wf[512 + 2 * (r1 * 16 + j0)] = y;
-                wf[512 + 2 * (r1 * 16 + j0) + 1] = shoup_pre(y, q);
-            }
-    };
-    {
-        unsigned nth = std::thread::hardware_concurrency();
-        if (nth < 1) nth = 1;
-        if (nth > T) nth = T;
-        if (nth > 16) nth = 16;
-        std::vector<std::thread> th;
-        for (unsigned w = 0; w < nth; w++)
-            th.emplace_back([&, w] {
-                for (u32 t = w; t < T; t += nth) build(t);
-            });
-        for (auto& x : th) x.join();
-    }
-    void* d = nullptr;
-    if (hipMalloc(&d, tab.size()) != hipSuccess) return false;
-    if (upload_blocking(d, tab.data(), tab.size()) != hipSuccess) {
-        (void)hipFree(d);
-        return false;
-    }
-    p->d_m16 = d;
-    p->m16_state = 1;
-    return true;
-}
-
-// the fused block pass: k_block_m16 or k_block_mma when the plan has their
-// tables (opt-in), else k_block
-static void launch_fused_block(ofhe_plan_t p, const PlanArgs& a, const u64* src, u64* dst, const u64* b, u32 batch,
-                               hipStream_t s) {
-    if (m16_ready(p)) {
-        const u32 T = p->towers, N = 1u << 16;
-        const unsigned char* base = reinterpret_cast<const unsigned char*>(p->d_m16);
-        M16Args Q;
-        Q.frag = reinterpret_cast<const i32x4*>(base);
-        Q.red = reinterpret_cast<const BmRed*>(base + (size_t)T * 2 * 1024 * 16);
-        Q.twf = reinterpret_cast<const u64*>(base + (size_t)T * 2 * 1024 * 16 + (size_t)T * sizeof(BmRed));
-        Q.w16 = Q.twf + (size_t)T * N * 2;
-        const u32 nwg = batch * T * 8;
-        hipLaunchKernelGGL(k_block_m16, dim3(nwg), dim3(M16_THREADS), 0, s, a, Q, src, dst, b, batch, nwg);
-        return;
-    }
-    if (!nm_ready(p)) {
-        launch_block<MODE_FUSED>(a, p->spq, src, dst, b, batch, s, p->split);
-        return;
-    }
-    NmArgs Q;
-    Q.frag = reinterpret_cast<const i32x4*>(p->d_nm);
-    Q.red = reinterpret_cast<const BmRed*>(reinterpret_cast<const unsigned char*>(p->d_nm) +
-                                           (size_t)p->towers * 256 * 2 * NM_FRAG * 16);
-    const u32 b16 = (batch + NM_POLYS - 1) / NM_POLYS * NM_POLYS;
-    Q.chunk = b16 < OFHE_NM_CHUNK ? b16 : OFHE_NM_CHUNK;
-    Q.nchunks = (batch + Q.chunk - 1) / Q.chunk;
-    const u32 nwg = p->towers * 256 * Q.nchunks;
-    hipLaunchKernelGGL(k_block_mma, dim3(nwg), dim3(NM_THREADS), 0, s, a, Q, src, dst, b, batch, nwg);
-}
-
-// k_pipe (pipe_kernels.hpp): the three passes as one persistent launch; its
-// queue heads and per-tower counters live in stream-ordered scratch
-static int launch_pipe(ofhe_plan_t p, const PlanArgs& a, const u64* a_, const u64* b, u64* c, u32 batch,
-                       hipStream_t s) {
-    const u64 units = (u64)batch * p->towers;
-    if (units * PIPE_PIECES >= (1ull << 32)) return fail(OFHE_ERR_ARG, "batch too large for the persistent pipeline");
-    const size_t words = (size_t)(2 * p->pipe_nq + 1) * PIPE_QSTRIDE + 2 * units;
-    void* ctl = nullptr;
-    hipError_t e = p->ctx->pool ? hipMallocFromPoolAsync(&ctl, words * 4, p->ctx->pool, s)
-                                : hipMallocAsync(&ctl, words * 4, s);
-    if (e != hipSuccess) return fail(OFHE_ERR_NOMEM, std::string("pipeline counters: ") + hipGetErrorString(e));
-    HIPCHK(hipMemsetAsync(ctl, 0, words * 4, s));
-    PipeCtl C;
-    C.head = (u32*)ctl;
-    C.members = C.head + (size_t)p->pipe_nq * PIPE_QSTRIDE;
-    C.exited = C.members + (size_t)p->pipe_nq * PIPE_QSTRIDE;
-    C.done_f = C.exited + PIPE_QSTRIDE;
-    C.done_b = C.done_f + units;
-    C.err = p->d_pipe_err;
-    C.units = (u32)units;
-    C.lag = p->pipe_lag;
-    C.nq = p->pipe_nq;
-    C.pieces = p->pipe_pieces;
-    C.wpq = p->pipe_static ? p->pipe_grid / p->pipe_nq : 0;
-#define LP(SP, HM) hipLaunchKernelGGL((k_pipe<SP, HM>), dim3(p->pipe_grid), dim3(256), 0, s, a, a_, c, b, batch, C)
-    if (!p->spq) {
-        LP(false, 1);  // generic moduli: one hand-off form
-    } else {
-        switch (p->pipe_hm) {
-            case 0: LP(true, 0); break;
-            case 2: LP(true, 2); break;
-            case 3: LP(true, 3); break;
-            default: LP(true, 1); break;
-        }
-    }
-#undef LP
-    HIPCHK(hipGetLastError());
-    HIPCHK(hipFreeAsync(ctl, s));
-    return post_launch();
-}
-
 int ofhe_hip_ntt_mul_intt(ofhe_plan_t p, const uint64_t* a_, const uint64_t* b, uint64_t* c,
                           uint32_t batch, void* stream) {
     int rc = check_common(p, batch);
@@ -1154,7 +785,6 @@ int ofhe_hip_ntt_mul_intt(ofhe_plan_t p, const uint64_t* a_, const uint64_t* b, 
         // one chunk's HBM-bound column passes overlap another's VALU-bound
         // block pass.
         const u32 cb = (p->chunk_batch && p->chunk_batch < batch) ? p->chunk_batch : batch;
-        if (p->pipe && cb == batch && !m16_ready(p) && !nm_ready(p)) return launch_pipe(p, a, a_, b, c, batch, s);
         const u64 words = (u64)p->towers << p->log_n;
         const bool multi = p->nstreams == 2 && cb < batch;
         // the fork / join events and side streams are the plan's: one caller at
@@ -1165,31 +795,15 @@ int ofhe_hip_ntt_mul_intt(ofhe_plan_t p, const uint64_t* a_, const uint64_t* b, 
             HIPCHK(hipEventRecord(p->ev_fork, s));
             for (int i = 0; i < 2; i++) HIPCHK(hipStreamWaitEvent(p->st[i], p->ev_fork, 0));
         }
-        // OFHE_CHUNK_SCRATCH: each stream's chunks pass their intermediates
-        // through one reused chunk-sized buffer, so those lines are rewritten
-        // in the Infinity Cache instead of landing on fresh addresses of c
-        void* scr[2] = {nullptr, nullptr};
-        const bool use_scr = p->chunk_scratch && cb < batch;
-        for (int i = 0; use_scr && i < (multi ? 2 : 1); i++) {
-            hipStream_t si = multi ? p->st[i] : s;
-            hipError_t e = p->ctx->pool ? hipMallocFromPoolAsync(&scr[i], (size_t)cb * words * 8, p->ctx->pool, si)
-                                        : hipMallocAsync(&scr[i], (size_t)cb * words * 8, si);
-            if (e != hipSuccess) {
-                for (int j = 0; j < i; j++) (void)hipFreeAsync(scr[j], multi ? p->st[j] : s);
-                return fail(OFHE_ERR_NOMEM, std::string("chunk scratch: ") + hipGetErrorString(e));
-            }
-        }
         u32 idx = 0;
         for (u32 b0 = 0; b0 < batch; b0 += cb, idx++) {
             const u32 n = batch - b0 < cb ? batch - b0 : cb;
             hipStream_t sx = multi ? p->st[idx & 1] : s;
             const u64 off = (u64)b0 * words;
-            u64* mid = use_scr ? (u64*)scr[multi ? (idx & 1) : 0] : c + off;
-            launch_colpass(a, p->spq, p->split, false, a_ + off, mid, n, sx);
-            launch_fused_block(p, a, mid, mid, b + off, n, sx);
-            launch_colpass(a, p->spq, p->split, true, mid, c + off, n, sx);
+            launch_colpass(a, p->spq, p->split, false, a_ + off, c + off, n, sx);
+            launch_block<MODE_FUSED>(a, p->spq, c + off, c + off, b + off, n, sx, p->split);
+            launch_colpass(a, p->spq, p->split, true, c + off, c + off, n, sx);
         }
-        for (int i = 0; use_scr && i < (multi ? 2 : 1); i++) (void)hipFreeAsync(scr[i], multi ? p->st[i] : s);
         if (multi) {
             for (int i = 0; i < 2; i++) {
                 HIPCHK(hipEventRecord(p->ev_join[i], p->st[i]));
@@ -1216,7 +830,7 @@ int ofhe_hip_ntt_mul_intt_stage(ofhe_plan_t p, int stage, const uint64_t* a_, co
     } else if (stage == 0) {
         launch_colpass(a, p->spq, p->split, false, a_, c, batch, s);
     } else if (stage == 1) {
-        launch_fused_block(p, a, c, c, b, batch, s);
+        launch_block<MODE_FUSED>(a, p->spq, c, c, b, batch, s, p->split);
     } else {
         launch_colpass(a, p->spq, p->split, true, c, c, batch, s);
     }
@@ -1426,7 +1040,16 @@ static bool bconv_mma_table(u32 size_q, u32 size_p, const u64* q, const u64* p, 
 int ofhe_hip_bconv_create(ofhe_ctx_t ctx, uint32_t log_n, uint32_t size_q, uint32_t size_p,
                           const uint64_t* q, const uint64_t* p, const uint64_t* qhat_inv_modq,
                           const uint64_t* qhat_modp, ofhe_bconv_t* out) {
+    return ofhe_hip_bconv_create_ex(ctx, log_n, size_q, size_p, q, p, qhat_inv_modq, qhat_modp, nullptr, out);
+}
+
+int ofhe_hip_bconv_create_ex(ofhe_ctx_t ctx, uint32_t log_n, uint32_t size_q, uint32_t size_p,
+                             const uint64_t* q, const uint64_t* p, const uint64_t* qhat_inv_modq,
+                             const uint64_t* qhat_modp, const ofhe_bconv_options* options, ofhe_bconv_t* out) {
     if (!ctx || !q || !p || !qhat_inv_modq || !qhat_modp || !out) return fail(OFHE_ERR_ARG, "NULL argument");
+    const ofhe_bconv_options opt = options ? *options : ofhe_bconv_options{};
+    if (opt.kernel > OFHE_BCONV_KERNEL_WIDE) return fail(OFHE_ERR_ARG, "options.kernel is not an OFHE_BCONV_KERNEL_* value");
+    if (opt.separate_cols > 1) return fail(OFHE_ERR_ARG, "options.separate_cols must be 0 or 1");
     if (log_n < 1 || log_n > 17) return fail(OFHE_ERR_ARG, "log_n must be in [1, 17]");
     if (size_q < 1 || size_p < 1 || size_q > 256 || size_p > 256)
         return fail(OFHE_ERR_ARG, "size_q and size_p must be in [1, 256]");
@@ -1480,10 +1103,7 @@ int ofhe_hip_bconv_create(ofhe_ctx_t ctx, uint32_t log_n, uint32_t size_q, uint3
     ofhe_bconv_s* b = new (std::nothrow) ofhe_bconv_s();
     if (!b) return fail(OFHE_ERR_NOMEM, "bconv allocation failed");
     b->ctx = ctx;
-    {
-        const char* e = getenv("OFHE_BCONV_COLS");
-        b->bcols = !(e && atoi(e) == 0);
-    }
+    b->bcols = !opt.separate_cols;
     hipError_t e = hipSetDevice(ctx->device);
     if (e == hipSuccess) e = hipMalloc(&b->d_mem, words_all * sizeof(u64));
     if (e == hipSuccess) e = upload_blocking(b->d_mem, h.data(), words_all * sizeof(u64));
@@ -1512,6 +1132,7 @@ int ofhe_hip_bconv_create(ofhe_ctx_t ctx, uint32_t log_n, uint32_t size_q, uint3
     A.mm_ks = mm_ks;
     A.mm_tpc = mm_tpc;
     A.mm_spq = mm_spq ? 1 : 0;
+    A.kernel = opt.kernel;
     *out = b;
     return OFHE_OK;
 }
@@ -1566,8 +1187,7 @@ int bconv_run(const BconvArgs& A, const u64* x, u64* out, u32 batch, hipStream_t
     const u64 total = (u64)batch << A.log_n;
     const u64 blocks = (total + 255) / 256;
     if (blocks >= (1ull << 31)) return fail(OFHE_ERR_ARG, "batch too large");
-    static const bool generic = getenv("OFHE_BCONV_GENERIC") != nullptr;  // A/B switches
-    static const bool limb = getenv("OFHE_BCONV_LIMB") != nullptr;
+    const bool generic = A.kernel == OFHE_BCONV_KERNEL_WIDE, limb = A.kernel == OFHE_BCONV_KERNEL_LIMB;
     if (OFHE_BCONV_MMA && A.mm_tab && A.log_n >= 5 && !generic && !limb) {
         const u64 groups = total >> 5;
         const u32 wpb = BCONV_MMA_THREADS / 64;

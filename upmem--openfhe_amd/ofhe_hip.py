@@ -65,9 +65,8 @@ _SIGS = {
                                             ctypes.POINTER(_vp)]),
     "ofhe_hip_plan_destroy": (ctypes.c_int, [_vp]),
     "ofhe_hip_plan_tune": (ctypes.c_int, [_vp, ctypes.c_uint32, ctypes.c_uint32]),
-    "ofhe_hip_plan_pipeline": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_uint32]),
-    "ofhe_hip_plan_pipeline_status": (ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_int),
-                                                     ctypes.POINTER(ctypes.c_uint32)]),
+    "ofhe_hip_plan_create_ex": (ctypes.c_int, [_vp, ctypes.c_uint32, ctypes.c_uint32, _u64p, _u64p,
+                                               _vp, ctypes.POINTER(_vp)]),
     "ofhe_hip_plan_tables": (ctypes.c_int, [_vp, _u64p, _u64p, _u64p, _u64p, _u64p]),
     "ofhe_hip_ntt_fwd": (ctypes.c_int, [_vp, _vp, ctypes.c_uint32, _vp]),
     "ofhe_hip_ntt_inv": (ctypes.c_int, [_vp, _vp, ctypes.c_uint32, _vp]),
@@ -83,6 +82,8 @@ _SIGS = {
     "ofhe_hip_ntt_mul_intt_stage": (ctypes.c_int, [_vp, ctypes.c_int, _vp, _vp, _vp, ctypes.c_uint32, _vp]),
     "ofhe_hip_bconv_create": (ctypes.c_int, [_vp, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
                                              _u64p, _u64p, _u64p, _u64p, ctypes.POINTER(_vp)]),
+    "ofhe_hip_bconv_create_ex": (ctypes.c_int, [_vp, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
+                                                _u64p, _u64p, _u64p, _u64p, _vp, ctypes.POINTER(_vp)]),
     "ofhe_hip_bconv_destroy": (ctypes.c_int, [_vp]),
     "ofhe_hip_approx_switch_crt_basis": (ctypes.c_int, [_vp, _vp, _vp, ctypes.c_uint32, _vp]),
     "ofhe_hip_ntt_fwd_range": (ctypes.c_int, [_vp, ctypes.c_uint32, ctypes.c_uint32, _vp, _vp, ctypes.c_uint64,
@@ -94,6 +95,9 @@ _SIGS = {
                                                 ctypes.c_uint32, _vp]),
     "ofhe_hip_ks_create": (ctypes.c_int, [_vp, ctypes.c_uint32, ctypes.c_uint32, _u64p, _u64p, ctypes.c_uint32,
                                           _u64p, _u64p, ctypes.c_uint32, ctypes.POINTER(_vp)]),
+    "ofhe_hip_ks_create_ex": (ctypes.c_int, [_vp, ctypes.c_uint32, ctypes.c_uint32, _u64p, _u64p,
+                                             ctypes.c_uint32, _u64p, _u64p, ctypes.c_uint32, _vp,
+                                             ctypes.POINTER(_vp)]),
     "ofhe_hip_ks_destroy": (ctypes.c_int, [_vp]),
     "ofhe_hip_ks_digits": (ctypes.c_int, [_vp, ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint32),
                                           ctypes.POINTER(ctypes.c_uint32)]),
@@ -161,6 +165,30 @@ def device_count() -> int:
     n = ctypes.c_int(0)
     _check(lib().ofhe_hip_device_count(ctypes.byref(n)))
     return n.value
+
+
+# Kernel-choice options of include/ofhe_hip.h (ofhe_plan_options,
+# ofhe_bconv_options, ofhe_ks_options).  Zero = the library's defaults; every
+# setting gives the same results (tests reach every kernel through them).
+SPLIT_AUTO, SPLIT_COLS, SPLIT_8_8, SPLIT_9_8, SPLIT_8_9 = range(5)
+BCONV_KERNEL_AUTO, BCONV_KERNEL_LIMB, BCONV_KERNEL_WIDE = range(3)
+
+
+class PlanOptions(ctypes.Structure):
+    _fields_ = [("split", ctypes.c_uint32), ("generic_moduli", ctypes.c_uint32)]
+
+
+class BconvOptions(ctypes.Structure):
+    _fields_ = [("kernel", ctypes.c_uint32), ("separate_cols", ctypes.c_uint32)]
+
+
+class KsOptions(ctypes.Structure):
+    _fields_ = [("plan", PlanOptions), ("separate_cols", ctypes.c_uint32), ("separate_icol", ctypes.c_uint32),
+                ("chunk", ctypes.c_uint32), ("single_stream", ctypes.c_uint32)]
+
+
+def _opt_ptr(o):
+    return None if o is None else ctypes.cast(ctypes.byref(o), _vp)
 
 
 class Context:
@@ -240,7 +268,8 @@ class NTTPlan:
     Data buffers are [batch][towers][N] uint64 residues in device memory.
     """
 
-    def __init__(self, ctx: Context, log_n: int, moduli: Sequence[int], roots: Sequence[int]):
+    def __init__(self, ctx: Context, log_n: int, moduli: Sequence[int], roots: Sequence[int],
+                 split: int = SPLIT_AUTO, generic_moduli: bool = False):
         if len(moduli) != len(roots):
             raise MathError("moduli and roots differ in length")
         self.ctx = ctx
@@ -250,8 +279,9 @@ class NTTPlan:
         self.roots = [int(r) for r in roots]
         self.towers = len(self.moduli)
         h = _vp()
-        _check(lib().ofhe_hip_plan_create(ctx.handle, self.log_n, self.towers, _arr(self.moduli),
-                                          _arr(self.roots), ctypes.byref(h)))
+        o = PlanOptions(int(split), 1 if generic_moduli else 0)
+        _check(lib().ofhe_hip_plan_create_ex(ctx.handle, self.log_n, self.towers, _arr(self.moduli),
+                                             _arr(self.roots), _opt_ptr(o), ctypes.byref(h)))
         self._h = h
 
     @property
@@ -274,18 +304,6 @@ class NTTPlan:
     def tune(self, chunk_batch: int = 0, streams: int = 1) -> None:
         """Chunking / stream knob of ntt_mul_intt (speed only; results are identical)."""
         _check(lib().ofhe_hip_plan_tune(self.handle, int(chunk_batch), int(streams)))
-
-    def pipeline(self, persistent: bool = True, lag: int = 0) -> None:
-        """Select the one-launch persistent ntt_mul_intt pipeline (log_n = 16) or the
-        three launches (speed only; results are identical).  Raises MathError when
-        the plan or the device cannot run it."""
-        _check(lib().ofhe_hip_plan_pipeline(self.handle, 1 if persistent else 0, int(lag)))
-
-    def pipeline_status(self):
-        """(persistent selected, waits given up so far); synchronises the device."""
-        on, faults = ctypes.c_int(), ctypes.c_uint32()
-        _check(lib().ofhe_hip_plan_pipeline_status(self.handle, ctypes.byref(on), ctypes.byref(faults)))
-        return bool(on.value), int(faults.value)
 
     def tables(self):
         """Host copies of (Table, TableP, TableI, TableIP, ninv) as flat lists."""
@@ -416,15 +434,17 @@ class BaseConverter:
     """ApproxSwitchCRTBasis from basis Q (size_q towers) to basis P (size_p towers)."""
 
     def __init__(self, ctx: Context, log_n: int, q: Sequence[int], p: Sequence[int],
-                 qhat_inv_modq: Sequence[int], qhat_modp: Sequence[int]):
+                 qhat_inv_modq: Sequence[int], qhat_modp: Sequence[int], kernel: int = BCONV_KERNEL_AUTO,
+                 separate_cols: bool = False):
         self.ctx = ctx
         self.log_n = int(log_n)
         self.size_q, self.size_p = len(q), len(p)
         if len(qhat_inv_modq) != self.size_q or len(qhat_modp) != self.size_q * self.size_p:
             raise MathError("precomputation sizes do not match the bases")
         h = _vp()
-        _check(lib().ofhe_hip_bconv_create(ctx.handle, self.log_n, self.size_q, self.size_p, _arr(q), _arr(p),
-                                           _arr(qhat_inv_modq), _arr(qhat_modp), ctypes.byref(h)))
+        o = BconvOptions(int(kernel), 1 if separate_cols else 0)
+        _check(lib().ofhe_hip_bconv_create_ex(ctx.handle, self.log_n, self.size_q, self.size_p, _arr(q), _arr(p),
+                                              _arr(qhat_inv_modq), _arr(qhat_modp), _opt_ptr(o), ctypes.byref(h)))
         self._h = h
 
     def close(self) -> None:
@@ -469,15 +489,16 @@ class KeySwitch:
     rq), special moduli p (roots rp) and num_part_q digits."""
 
     def __init__(self, ctx: Context, log_n: int, q: Sequence[int], rq: Sequence[int], p: Sequence[int],
-                 rp: Sequence[int], num_part_q: int):
+                 rp: Sequence[int], num_part_q: int, options: "KsOptions" = None):
         self.ctx = ctx
         self.log_n, self.n = int(log_n), 1 << int(log_n)
         self.q, self.p = [int(v) for v in q], [int(v) for v in p]
         self.size_q, self.size_p = len(self.q), len(self.p)
         self.num_part_q = int(num_part_q)
         h = _vp()
-        _check(lib().ofhe_hip_ks_create(ctx.handle, self.log_n, self.size_q, _arr(q), _arr(rq), self.size_p,
-                                        _arr(p), _arr(rp), self.num_part_q, ctypes.byref(h)))
+        self.options = options
+        _check(lib().ofhe_hip_ks_create_ex(ctx.handle, self.log_n, self.size_q, _arr(q), _arr(rq), self.size_p,
+                                           _arr(p), _arr(rp), self.num_part_q, _opt_ptr(options), ctypes.byref(h)))
         self._h = h
 
     def close(self) -> None:
