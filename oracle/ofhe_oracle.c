@@ -463,6 +463,26 @@ void oracle_base_conv_precompute(unsigned sizeQ, unsigned sizeP, const u64* q, c
     }
 }
 
+/* PolyImpl::AutomorphismTransform(k), X -> X^k for odd k, one tower of n
+ * words (src/core/include/lattice/hal/default/poly-impl.h:312-365):
+ * evaluation form permutes the bit-reversed slots, out[rev(j)] =
+ * x[rev(((j*2k + k) mod 2^32 >> 1) & (n-1))]; coefficient form maps
+ * coefficient j to (j*k) mod n, negated (q - x, so a zero becomes q as in the
+ * reference) when bit log n of the 32-bit j*k is set.  k must be odd. */
+void oracle_automorphism(const u64* x, u64* out, u64 n, uint32_t k, int eval_form, u64 q) {
+    const unsigned logn = oracle_msb(n) - 1;
+    const uint32_t mask = (uint32_t)n - 1;
+    if (eval_form) {
+        uint32_t jk = k;
+        for (uint32_t j = 0; j < (uint32_t)n; j++, jk += 2 * k)
+            out[rev_bits(j, logn)] = x[rev_bits((jk >> 1) & mask, logn)];
+        return;
+    }
+    uint32_t jk = 0;
+    for (uint32_t j = 0; j < (uint32_t)n; j++, jk += k)
+        out[jk & mask] = ((jk >> logn) & 1u) ? q - x[j] : x[j];
+}
+
 /* ---------------------------------------------------------------------------
  * Deterministic synthetic inputs and fingerprints.
  * ------------------------------------------------------------------------- */

@@ -5,7 +5,9 @@
 #include <cstdio>
 #include <cstdlib>
 #include <functional>
+#include <cstring>
 #include <random>
+#include <sstream>
 #include <string>
 #include <thread>
 #include <vector>
@@ -743,6 +745,52 @@ static void register_tests() {
         EXPECT_EQ(viaCache.second, direct.second, "ct1");
         KeyCache::erase("relin");
         EXPECT_THROW(KeyCache::get("relin"), math_error, "erased key");
+    });
+    // Save / Load in the reference's DCRTPoly field order (dcrtpoly.h:349-365,
+    // poly.h:322-338, mubintvecnat.h:665-713): a round trip of a batch, the
+    // record layout, and deserialize_error on corrupt input
+    TEST("DCRTPolyHip.save_load_round_trip", [] {
+        const uint32_t m = 1u << 13, n = m / 2, T = 3, batch = 2;
+        std::vector<uint64_t> q;
+        uint64_t x = first_prime(60, m);
+        for (uint32_t t = 0; t < T; t++) q.push_back(x = previous_prime(x, m));
+        auto P = params(m, q);
+        std::mt19937_64 rng(41);
+        std::vector<uint64_t> v((size_t)batch * T * n);
+        for (size_t i = 0; i < v.size(); i++) v[i] = rng() % q[(i / n) % T];
+        for (Format f : {Format::EVALUATION, Format::COEFFICIENT}) {
+            DCRTPolyHip X(P, f, batch);
+            X.SetValues(v, f);
+            std::stringstream ss;
+            X.Save(ss);
+            const std::string bytes = ss.str();
+            // per record: T, per tower (N, N words, q, format, co, rd, q, root), format, co, rd, T, T x params
+            const size_t rec = 8 + T * (8 + 8 * (size_t)n + 8 + 4 + 24) + 4 + 4 + 4 + 8 + T * 24;
+            EXPECT_EQ(bytes.size(), batch * rec, "record size");
+            uint64_t w[3];
+            std::memcpy(w, bytes.data(), 24);
+            EXPECT_EQ(w[0], (uint64_t)T, "towers first (\"v\" = m_vectors)");
+            EXPECT_EQ(w[1], (uint64_t)n, "then the first tower's value count");
+            EXPECT_EQ(w[2], v[0], "then its first value");
+            DCRTPolyHip Y = DCRTPolyHip::Load(ss, batch);
+            EXPECT_EQ(Y.GetFormat() == f, true, "format restored");
+            EXPECT_EQ(Y.GetParams()->Moduli(), q, "moduli restored");
+            EXPECT_EQ(Y.GetParams()->Roots(), P->Roots(), "roots restored");
+            EXPECT_EQ(Y, X, "values restored");
+            // corrupt: a value >= q, a truncated stream
+            std::string bad = bytes;
+            const uint64_t big = q[0];
+            std::memcpy(&bad[16], &big, 8);
+            std::stringstream sb(bad), st(bytes.substr(0, bytes.size() - 5));
+            EXPECT_THROW(DCRTPolyHip::Load(sb, batch), deserialize_error, "non-canonical value");
+            EXPECT_THROW(DCRTPolyHip::Load(st, batch), deserialize_error, "truncated stream");
+        }
+        // two records over different bases cannot form one batch
+        std::stringstream mix;
+        DCRTPolyHip A(P, Format::EVALUATION), B(params(m, std::vector<uint64_t>(q.begin(), q.begin() + 2)), Format::EVALUATION);
+        A.Save(mix);
+        B.Save(mix);
+        EXPECT_THROW(DCRTPolyHip::Load(mix, 2), deserialize_error, "mixed bases in one batch");
     });
     TEST("DCRTPolyHip.errors", [] {
         auto P = params(16, {first_prime(22, 16)});

@@ -29,7 +29,9 @@
 #include <algorithm>
 #include <cstdint>
 #include <cstring>
+#include <istream>
 #include <map>
+#include <ostream>
 #include <memory>
 #include <mutex>
 #include <stdexcept>
@@ -48,6 +50,10 @@ public:
 class not_implemented_error : public std::runtime_error {
 public:
     explicit not_implemented_error(const std::string& m) : std::runtime_error(m) {}
+};
+class deserialize_error : public std::runtime_error {  // lbcrypto::deserialize_error (utils/exception.h)
+public:
+    explicit deserialize_error(const std::string& m) : std::runtime_error(m) {}
 };
 
 inline void check(int rc, const char* what) {
@@ -471,7 +477,118 @@ public:
         return f_ == o.f_ && p_->Moduli() == o.p_->Moduli() && GetValues() == o.GetValues();
     }
 
+    // Serialization in the reference's field order, one DCRTPoly record per
+    // batch entry:
+    //   DCRTPolyImpl::save (dcrtpoly.h:349-354): "v" towers, "f" format, "p" params
+    //   PolyImpl::save (poly.h:322-327):         "v" values, "f" format, "p" params
+    //   NativeVectorT::save, binary (mubintvecnat.h:665-674): size_type count, the
+    //     words as binary_data, then the modulus (one NativeInteger word)
+    //   ElemParams::save (elemparams.h:224-231): "co", "rd", "cm", "ru"
+    //   ILDCRTParams::save (ildcrtparams.h:351-355): its ElemParams, then "p" the
+    //     per-tower ILNativeParams
+    // Little-endian, with cereal's binary conventions for what the reference
+    // writes itself: a uint64 size_type before every vector, enums as uint32
+    // (Format, utils/inttypes.h:65).  Not written: cereal's own framing
+    // (class-version words, shared_ptr ids, the polymorphic params' type
+    // names) and the BigInteger fields ("bm", "br", ILDCRTParams' "m"); cereal
+    // is an empty submodule in the reference snapshot, so its byte stream is
+    // not reproduced or pinned here.
+    void Save(std::ostream& os) const {
+        const auto h = GetValues();
+        const size_t T = p_->Towers(), n = p_->GetRingDimension();
+        const uint32_t co = p_->GetCyclotomicOrder(), rd = p_->GetRingDimension();
+        for (uint32_t b = 0; b < batch_; b++) {
+            put<uint64_t>(os, T);
+            for (size_t t = 0; t < T; t++) {
+                put<uint64_t>(os, n);
+                os.write(reinterpret_cast<const char*>(h.data() + ((size_t)b * T + t) * n), n * 8);
+                put<uint64_t>(os, p_->Moduli()[t]);
+                put<uint32_t>(os, (uint32_t)f_);
+                put_native_params(os, co, rd, p_->Moduli()[t], p_->Roots()[t]);
+            }
+            put<uint32_t>(os, (uint32_t)f_);
+            put<uint32_t>(os, co);
+            put<uint32_t>(os, rd);
+            put<uint64_t>(os, T);
+            for (size_t t = 0; t < T; t++) put_native_params(os, co, rd, p_->Moduli()[t], p_->Roots()[t]);
+        }
+        if (!os) throw math_error("DCRTPolyHip::Save: stream write failed");
+    }
+    // The inverse of Save for `batch` consecutive records; every record must
+    // carry the same basis and format, and every value must be canonical.
+    static DCRTPolyHip Load(std::istream& is, uint32_t batch = 1, int device = 0) {
+        if (batch == 0) throw deserialize_error("DCRTPolyHip::Load: batch must be >= 1");
+        std::vector<uint64_t> flat, q0, r0;
+        uint32_t co0 = 0, f0 = 0;
+        for (uint32_t b = 0; b < batch; b++) {
+            const uint64_t T = get<uint64_t>(is);
+            if (T < 1 || T > 4096) throw deserialize_error("DCRTPolyHip::Load: tower count out of range");
+            std::vector<uint64_t> q(T), r(T), vals;
+            uint32_t co = 0, f = 0;
+            for (uint64_t t = 0; t < T; t++) {
+                const uint64_t n = get<uint64_t>(is);
+                if (n < 2 || n > (1u << 17) || (n & (n - 1))) throw deserialize_error("DCRTPolyHip::Load: ring dimension");
+                const size_t off = vals.size();
+                vals.resize(off + n);
+                is.read(reinterpret_cast<char*>(vals.data() + off), n * 8);
+                const uint64_t m = get<uint64_t>(is);
+                const uint32_t tf = get<uint32_t>(is);
+                uint32_t tco, trd;
+                uint64_t tq, tr;
+                get_native_params(is, tco, trd, tq, tr);
+                if (tq != m || trd != n || tco != 2 * n) throw deserialize_error("DCRTPolyHip::Load: tower params disagree");
+                if (t == 0) co = tco, f = tf;
+                if (tco != co || tf != f) throw deserialize_error("DCRTPolyHip::Load: towers of different rings / formats");
+                for (size_t i = off; i < off + n; i++)
+                    if (vals[i] >= m) throw deserialize_error("DCRTPolyHip::Load: value not below its modulus");
+                q[t] = m;
+                r[t] = tr;
+            }
+            const uint32_t pf = get<uint32_t>(is), pco = get<uint32_t>(is), prd = get<uint32_t>(is);
+            const uint64_t pT = get<uint64_t>(is);
+            if (pf != f || pco != co || prd != co / 2 || pT != T) throw deserialize_error("DCRTPolyHip::Load: params disagree");
+            for (uint64_t t = 0; t < T; t++) {
+                uint32_t tco, trd;
+                uint64_t tq, tr;
+                get_native_params(is, tco, trd, tq, tr);
+                if (tco != co || tq != q[t] || tr != r[t]) throw deserialize_error("DCRTPolyHip::Load: params disagree");
+            }
+            if (f > 1) throw deserialize_error("DCRTPolyHip::Load: unknown format");
+            if (b == 0) q0 = q, r0 = r, co0 = co, f0 = f;
+            if (q != q0 || r != r0 || co != co0 || f != f0)
+                throw deserialize_error("DCRTPolyHip::Load: batch entries over different bases / formats");
+            flat.insert(flat.end(), vals.begin(), vals.end());
+        }
+        auto P = std::make_shared<DCRTParams>(co0, q0, r0, device);
+        DCRTPolyHip x(P, (Format)f0, batch, Uninit{});
+        x.SetValues(flat, (Format)f0);
+        return x;
+    }
+
 private:
+    template <class T>
+    static void put(std::ostream& os, T v) {
+        os.write(reinterpret_cast<const char*>(&v), sizeof v);  // little-endian host (x86-64)
+    }
+    template <class T>
+    static T get(std::istream& is) {
+        T v{};
+        if (!is.read(reinterpret_cast<char*>(&v), sizeof v)) throw deserialize_error("DCRTPolyHip::Load: truncated stream");
+        return v;
+    }
+    // ILNativeParams = ElemParams' "co", "rd", "cm" (the tower modulus), "ru"
+    static void put_native_params(std::ostream& os, uint32_t co, uint32_t rd, uint64_t q, uint64_t r) {
+        put<uint32_t>(os, co);
+        put<uint32_t>(os, rd);
+        put<uint64_t>(os, q);
+        put<uint64_t>(os, r);
+    }
+    static void get_native_params(std::istream& is, uint32_t& co, uint32_t& rd, uint64_t& q, uint64_t& r) {
+        co = get<uint32_t>(is);
+        rd = get<uint32_t>(is);
+        q = get<uint64_t>(is);
+        r = get<uint64_t>(is);
+    }
     // DropLastElement (dcrtpoly-impl.h:719-728): the params of the chain
     // without its last tower (a cached plan of that basis)
     std::shared_ptr<DCRTParams> lower_params() const {

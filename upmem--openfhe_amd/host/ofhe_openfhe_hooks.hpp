@@ -20,8 +20,14 @@
 //   DCRTPolyImpl::operator*= / Times    dcrtpoly.h:142-148, 185-200 -> TimesEq(m_vectors, rhs.m_vectors)
 //   DCRTPolyImpl::operator+= / -=       dcrtpoly-impl.h:410-416     -> PlusEq / MinusEq
 //   DCRTPolyImpl::ApproxSwitchCRTBasis  dcrtpoly-impl.h:1034-1063   -> ApproxSwitchCRTBasis(...)
+//   DCRTPolyImpl::ApproxModUp           dcrtpoly-impl.h:1084-1131   -> ApproxModUp(m_vectors, sizeQ, ...)
+//   DCRTPolyImpl::ApproxModDown         dcrtpoly-impl.h:1133-1175   -> ApproxModDown(m_vectors, ans.m_vectors, ...)
+//   DCRTPolyImpl::AutomorphismTransform dcrtpoly-impl.h:349-357     -> AutomorphismTransform(m_vectors, result.m_vectors, k)
+//   DCRTPolyImpl::Times / operator*= by scalar   dcrtpoly-impl.h:586-661 -> TimesScalarEq / TimesSignedEq
+//   DCRTPolyImpl::Minus by scalar       dcrtpoly-impl.h:565-584     -> MinusScalarEq
 #pragma once
 
+#include <algorithm>
 #include <cstdint>
 #include <map>
 #include <memory>
@@ -166,40 +172,52 @@ void MinusEq(Towers& a, const Towers& b, int device = 0) {
     detail::binary_eq(a, b, 2, "hooks::MinusEq", device);
 }
 
+// NTT plan over towers [t0, t0 + count) of a view (PlanCache: one per basis)
+inline std::shared_ptr<PlanHandle> plan_of(const TowerView& v, size_t t0, size_t count, int device) {
+    std::vector<uint64_t> q(v.q.begin() + t0, v.q.begin() + t0 + count);
+    std::vector<uint64_t> r(v.psi.begin() + t0, v.psi.begin() + t0 + count);
+    return PlanCache::get(device, v.log_n, q, r);
+}
+
+// Base converter src -> dst with the pke layer's tables (rns-cryptoparameters.cpp
+// :273-337; hmod row-major [src][dst]), built once per (basis pair, tables) and
+// cached process-wide, as the reference precomputes them once per parameter set.
+inline std::shared_ptr<ofhe_bconv_s> converter(int device, uint32_t log_n, const std::vector<uint64_t>& src,
+                                               const std::vector<uint64_t>& dst, const std::vector<uint64_t>& hinv,
+                                               const std::vector<uint64_t>& hmod, const char* what) {
+    if (hinv.size() != src.size() || hmod.size() != src.size() * dst.size())
+        throw math_error(std::string(what) + ": table sizes");
+    HipManager* m = HipManager::getHip(device);
+    static std::mutex mu;
+    static std::map<std::vector<uint64_t>, std::shared_ptr<ofhe_bconv_s>> cache;
+    std::vector<uint64_t> key{(uint64_t)device, log_n, src.size()};
+    key.insert(key.end(), src.begin(), src.end());
+    key.insert(key.end(), dst.begin(), dst.end());
+    key.insert(key.end(), hinv.begin(), hinv.end());
+    key.insert(key.end(), hmod.begin(), hmod.end());
+    std::lock_guard<std::mutex> lk(mu);
+    auto& e = cache[key];
+    if (!e) {
+        ofhe_bconv_t h = nullptr;
+        check(ofhe_hip_bconv_create(m->ctx(), log_n, (uint32_t)src.size(), (uint32_t)dst.size(), src.data(), dst.data(),
+                                    hinv.data(), hmod.data(), &h),
+              what);
+        e = std::shared_ptr<ofhe_bconv_s>(h, [](ofhe_bconv_t p) { ofhe_hip_bconv_destroy(p); });
+    }
+    return e;
+}
+
 // DCRTPolyImpl::ApproxSwitchCRTBasis (dcrtpoly-impl.h:1034-1063): x's towers
 // (basis Q, COEFFICIENT form) -> out's towers (basis P, already sized by the
 // caller as the reference's `ans(paramsP, m_format, true)`), with the
 // QHatInvModq / QHatModp tables the pke layer precomputes
 // (rns-cryptoparameters.cpp:273-337; QHatModp row-major [sizeQ][sizeP]).
-// The converter is built once per (Q, P) and cached.
 template <class TowersQ, class TowersP>
 void ApproxSwitchCRTBasis(const TowersQ& x, TowersP& out, const std::vector<uint64_t>& QHatInvModq,
                           const std::vector<uint64_t>& QHatModp, int device = 0) {
     TowerView vx = view(const_cast<TowersQ&>(x)), vo = view(out);
     if (vx.n != vo.n) throw math_error("hooks::ApproxSwitchCRTBasis: ring dimensions differ");
-    if (QHatInvModq.size() != vx.q.size() || QHatModp.size() != vx.q.size() * vo.q.size())
-        throw math_error("hooks::ApproxSwitchCRTBasis: table sizes");
-    HipManager* m = HipManager::getHip(device);
-    static std::mutex mu;  // the converter cache is process-wide
-    static std::map<std::vector<uint64_t>, std::shared_ptr<ofhe_bconv_s>> cache;
-    std::shared_ptr<ofhe_bconv_s> bc;
-    {
-        std::vector<uint64_t> key{(uint64_t)device, vx.log_n, vx.q.size()};
-        key.insert(key.end(), vx.q.begin(), vx.q.end());
-        key.insert(key.end(), vo.q.begin(), vo.q.end());
-        key.insert(key.end(), QHatInvModq.begin(), QHatInvModq.end());
-        key.insert(key.end(), QHatModp.begin(), QHatModp.end());
-        std::lock_guard<std::mutex> lk(mu);
-        auto& e = cache[key];
-        if (!e) {
-            ofhe_bconv_t h = nullptr;
-            check(ofhe_hip_bconv_create(m->ctx(), vx.log_n, (uint32_t)vx.q.size(), (uint32_t)vo.q.size(), vx.q.data(),
-                                        vo.q.data(), QHatInvModq.data(), QHatModp.data(), &h),
-                  "hooks::ApproxSwitchCRTBasis");
-            e = std::shared_ptr<ofhe_bconv_s>(h, [](ofhe_bconv_t p) { ofhe_hip_bconv_destroy(p); });
-        }
-        bc = e;
-    }
+    auto bc = converter(device, vx.log_n, vx.q, vo.q, QHatInvModq, QHatModp, "hooks::ApproxSwitchCRTBasis");
     const size_t wx = vx.q.size() * (size_t)vx.n, wo = vo.q.size() * (size_t)vo.n;
     Staging& sx = staging(device, wx, 0);
     Staging& so = staging(device, wo, 1);
@@ -208,6 +226,149 @@ void ApproxSwitchCRTBasis(const TowersQ& x, TowersP& out, const std::vector<uint
     check(ofhe_hip_approx_switch_crt_basis(bc.get(), sx.dev(), so.dev(), 1, nullptr), "hooks::ApproxSwitchCRTBasis");
     so.download(wo);
     so.scatter(vo.data, vo.n);
+}
+
+// DCRTPolyImpl::ApproxModUp (dcrtpoly-impl.h:1084-1131).  `towers` is
+// m_vectors after the caller's resize to Q|P: the sizeQ towers of x (all in
+// one format) followed by sizeP towers whose params are paramsP's (their
+// values are ignored).  On return every tower holds ApproxModUp(x) in
+// EVALUATION form -- the Q towers x itself in evaluation form, the P towers
+// NTT(ApproxSwitchCRTBasis(x)) -- and says so (OverrideFormat), as the
+// reference's m_format = EVALUATION, m_params = paramsQP leave it.
+template <class Towers>
+void ApproxModUp(Towers& towers, size_t sizeQ, const std::vector<uint64_t>& QHatInvModq,
+                 const std::vector<uint64_t>& QHatModp, int device = 0) {
+    using Fmt = std::decay_t<decltype(towers[0].GetFormat())>;
+    if (sizeQ < 1 || sizeQ >= towers.size()) throw math_error("hooks::ApproxModUp: sizeQ outside (0, towers)");
+    const bool eval = towers[0].GetFormat() == Fmt::EVALUATION;
+    for (size_t i = 0; i < sizeQ; i++)
+        if (towers[i].GetFormat() != towers[0].GetFormat()) throw math_error("hooks::ApproxModUp: mixed formats");
+    TowerView v = view(towers);
+    const size_t sizeP = v.q.size() - sizeQ;
+    auto pq = plan_of(v, 0, sizeQ, device), pp = plan_of(v, sizeQ, sizeP, device);
+    std::vector<uint64_t> q(v.q.begin(), v.q.begin() + sizeQ), p(v.q.begin() + sizeQ, v.q.end());
+    auto bc = converter(device, v.log_n, q, p, QHatInvModq, QHatModp, "hooks::ApproxModUp");
+    const size_t wx = sizeQ * (size_t)v.n, wo = v.q.size() * (size_t)v.n;
+    Staging& sx = staging(device, wx, 0);
+    Staging& so = staging(device, wo, 1);
+    sx.gather(cptr(std::vector<uint64_t*>(v.data.begin(), v.data.begin() + sizeQ)), v.n);
+    sx.upload(wx);
+    check(ofhe_hip_approx_mod_up(pq->get(), pp->get(), bc.get(), eval ? 1 : 0, sx.dev(), so.dev(), 1, nullptr),
+          "hooks::ApproxModUp");
+    so.download(wo);
+    so.scatter(v.data, v.n);
+    for (auto& t : towers) t.OverrideFormat(Fmt::EVALUATION);
+}
+
+// DCRTPolyImpl::ApproxModDown (dcrtpoly-impl.h:1133-1175): x = the Q|P towers
+// in EVALUATION form -> out, the caller's `ans` (sizeQ = out.size() towers over
+// paramsQ, after its DropLastElements), in EVALUATION form:
+//   out_i = (x_i - NTT(t * ApproxSwitchCRTBasis_{P->Q}(t^-1 * INTT(x_P)))_i) * PInvModq_i
+// with the t factors only when t > 0 (BGV; the reference's tInvModp is
+// t.ModInverse(p_j), bgvrns-cryptoparameters.cpp:83-88, derived here from t).
+// PHatInvModp / PHatModq ([sizeP][sizeQ]) as rns-cryptoparameters.cpp:172-215.
+template <class TowersQP, class TowersQ>
+void ApproxModDown(const TowersQP& x, TowersQ& out, const std::vector<uint64_t>& PInvModq,
+                   const std::vector<uint64_t>& PHatInvModp, const std::vector<uint64_t>& PHatModq, uint64_t t = 0,
+                   int device = 0) {
+    using Fmt = std::decay_t<decltype(x[0].GetFormat())>;
+    for (const auto& tw : x)
+        if (tw.GetFormat() != Fmt::EVALUATION) throw math_error("hooks::ApproxModDown: EVALUATION form expected");
+    TowerView vx = view(const_cast<TowersQP&>(x)), vo = view(out);
+    const size_t sizeQ = vo.q.size();
+    if (sizeQ >= vx.q.size()) throw math_error("hooks::ApproxModDown: output has as many towers as the input");
+    if (!std::equal(vo.q.begin(), vo.q.end(), vx.q.begin()) || vo.n != vx.n)
+        throw math_error("hooks::ApproxModDown: output basis is not the input's Q part");
+    if (PInvModq.size() != sizeQ) throw math_error("hooks::ApproxModDown: PInvModq size");
+    const size_t sizeP = vx.q.size() - sizeQ;
+    auto pq = plan_of(vx, 0, sizeQ, device), pp = plan_of(vx, sizeQ, sizeP, device);
+    std::vector<uint64_t> q(vx.q.begin(), vx.q.begin() + sizeQ), p(vx.q.begin() + sizeQ, vx.q.end());
+    auto bc = converter(device, vx.log_n, p, q, PHatInvModp, PHatModq, "hooks::ApproxModDown");
+    const size_t wx = vx.q.size() * (size_t)vx.n, wo = sizeQ * (size_t)vx.n;
+    Staging& sx = staging(device, wx, 0);
+    Staging& so = staging(device, wo, 1);
+    sx.gather(cptr(vx.data), vx.n);
+    sx.upload(wx);
+    check(ofhe_hip_approx_mod_down(pq->get(), pp->get(), bc.get(), PInvModq.data(), t, sx.dev(), so.dev(), 1,
+                                   nullptr),
+          "hooks::ApproxModDown");
+    so.download(wo);
+    so.scatter(vo.data, vo.n);
+    for (auto& tw : out) tw.OverrideFormat(Fmt::EVALUATION);
+}
+
+// DCRTPolyImpl::AutomorphismTransform(k) (dcrtpoly-impl.h:349-357 ->
+// PolyImpl::AutomorphismTransform, poly-impl.h:312-365): out (the caller's
+// result, same params and size as x) = sigma_k(x) tower by tower, in x's
+// format (evaluation: bit-reversed slot permutation; coefficient: signed
+// permutation).  An even k throws math_error as the reference does.
+template <class Towers>
+void AutomorphismTransform(const Towers& x, Towers& out, uint32_t k, int device = 0) {
+    using Fmt = std::decay_t<decltype(x[0].GetFormat())>;
+    const bool eval = x[0].GetFormat() == Fmt::EVALUATION;
+    for (const auto& tw : x)
+        if (tw.GetFormat() != x[0].GetFormat()) throw math_error("hooks::AutomorphismTransform: mixed formats");
+    TowerView vx = view(const_cast<Towers&>(x)), vo = view(out);
+    if (vx.q != vo.q || vx.n != vo.n) throw math_error("hooks::AutomorphismTransform: output basis differs");
+    auto plan = plan_of(vx, 0, vx.q.size(), device);
+    const size_t words = vx.q.size() * (size_t)vx.n;
+    Staging& sx = staging(device, words, 0);
+    Staging& so = staging(device, words, 1);
+    sx.gather(cptr(vx.data), vx.n);
+    sx.upload(words);
+    check(ofhe_hip_automorphism(plan->get(), k, eval ? 1 : 0, sx.dev(), so.dev(), 1, nullptr),
+          "hooks::AutomorphismTransform");
+    so.download(words);
+    so.scatter(vo.data, vo.n);
+    for (auto& tw : out) tw.OverrideFormat(x[0].GetFormat());
+}
+
+namespace detail {
+// x_t (op)= s_t over all towers in one launch; op 0 ModMul (Shoup), 2 ModSub
+template <class Towers>
+void scalar_eq(Towers& x, const std::vector<uint64_t>& s, int op, const char* what, int device) {
+    TowerView v = view(x);
+    if (s.size() != v.q.size()) throw math_error(std::string(what) + ": one scalar per tower required");
+    auto plan = plan_of(v, 0, v.q.size(), device);
+    const size_t words = v.q.size() * (size_t)v.n;
+    Staging& st = staging(device, words, 0);
+    st.gather(cptr(v.data), v.n);
+    st.upload(words);
+    check(op == 0 ? ofhe_hip_modmul_scalar(plan->get(), st.dev(), s.data(), st.dev(), 1, nullptr)
+                  : ofhe_hip_modsub_scalar(plan->get(), st.dev(), s.data(), st.dev(), 1, nullptr),
+          what);
+    st.download(words);
+    st.scatter(v.data, v.n);
+}
+}  // namespace detail
+
+// DCRTPolyImpl::Times(const std::vector<NativeInteger>&) / Times(Integer) /
+// operator*=(NativeInteger) (dcrtpoly-impl.h:586-661 -> PolyImpl::Times,
+// NativeVectorT::ModMul(Eq)(const IntegerType&), mubintvecnat.cpp:310-332):
+// tower t times s[t] mod q_t, in place (the caller copies first for Times).
+template <class Towers>
+void TimesScalarEq(Towers& x, const std::vector<uint64_t>& s, int device = 0) {
+    detail::scalar_eq(x, s, 0, "hooks::TimesScalarEq", device);
+}
+// DCRTPolyImpl::Times(NativeInteger::SignedNativeInt) (dcrtpoly-impl.h:597-605
+// -> PolyImpl::Times, poly-impl.h:237-252): a negative v multiplies by
+// q - (|v| mod q) in every tower.
+template <class Towers>
+void TimesSignedEq(Towers& x, int64_t v, int device = 0) {
+    std::vector<uint64_t> s;
+    for (auto& tw : x) {
+        const uint64_t q = (uint64_t)tw.GetParams()->GetModulus().ConvertToInt();
+        const uint64_t mag = v < 0 ? (uint64_t)0 - (uint64_t)v : (uint64_t)v;  // |v| without overflow at INT64_MIN
+        s.push_back(v < 0 ? q - mag % q : mag);                              // q - 0 = q reduces to 0
+    }
+    detail::scalar_eq(x, s, 0, "hooks::TimesSignedEq", device);
+}
+// DCRTPolyImpl::Minus(const Integer&) / Minus(const std::vector<Integer>&)
+// (dcrtpoly-impl.h:565-584 -> PolyImpl::Minus, poly-impl.h:223-227): every word
+// of tower t minus s[t] mod q_t, in either format.
+template <class Towers>
+void MinusScalarEq(Towers& x, const std::vector<uint64_t>& s, int device = 0) {
+    detail::scalar_eq(x, s, 2, "hooks::MinusScalarEq", device);
 }
 
 }  // namespace hooks
