@@ -198,3 +198,57 @@ def test_two_rank_unique_id_failure_falls_back_without_hanging():
     for rank, fell_back, label, key_ok in res:
         assert fell_back and key_ok, res
         assert "torch.distributed gloo" in label and "unique id failed on rank 0" in label, label
+
+
+def _tower_worker(rank, world, port, q):
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        try:
+            import oracle as O
+
+            # configs[3] in miniature: 32 towers split into contiguous ranges
+            # over the ranks (shard.shard_towers, bench.py --shard towers /
+            # bench_configs3), each rank's plan over its own sub-basis of the
+            # global chain; inputs drawn per GLOBAL tower index.  The oracle
+            # stands in for the device compute on CPU.
+            log_n, T, B = 8, 32, 2
+            n = 1 << log_n
+            qs, rs = O.moduli_chain(log_n, T)
+            a = O.uniform_dcrt(B, T, n, qs, 31)
+            b = O.uniform_dcrt(B, T, n, qs, 32)
+            t0, cnt = shard.shard_towers(T, rank, world)
+            local = O.ntt_mul_intt(a[:, t0:t0 + cnt], b[:, t0:t0 + cnt], O.Tables(n, qs[t0:t0 + cnt], rs[t0:t0 + cnt]))
+            parts = [None] * world
+            dist.all_gather_object(parts, (t0, local))  # test-side check only: the product path has no gather
+            parts.sort(key=lambda x: x[0])
+            got = np.concatenate([p[1] for p in parts], axis=1)
+            want = O.ntt_mul_intt(a, b, O.Tables(n, qs, rs))
+            q.put((rank, bool(got.shape == want.shape and np.array_equal(got, want)),
+                   [p[0] for p in parts]))
+        finally:
+            dist.destroy_process_group()
+    except Exception as e:
+        q.put((rank, repr(e), None))
+        raise
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_tower_sharded_pipeline_matches_single_rank(world):
+    """configs[3]: T = 32 towers split over `world` ranks (16 + 16; 11 + 11 + 10),
+    every rank's tower range through the pipeline on its own sub-basis, the
+    shards gathered along the tower axis equal the single-rank result bit for
+    bit."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_tower_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=180) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert all(r[1] is True for r in res), res
+    starts = [shard.shard_towers(32, r, world)[0] for r in range(world)]
+    assert all(r[2] == starts for r in res)
