@@ -279,9 +279,10 @@ def ternary(n, rng):
 def small_poly_eval(coeffs, moduli, roots):
     """signed small coefficients -> [1][T][N] evaluation form."""
     n = len(coeffs)
+    c = np.asarray(coeffs, dtype=np.int64)  # |coeffs| small; every modulus < 2^60 fits int64
     x = np.empty((1, len(moduli), n), np.uint64)
     for t, m in enumerate(moduli):
-        x[0, t] = np.array([int(v) % int(m) for v in coeffs], dtype=np.uint64)
+        x[0, t] = (c % np.int64(int(m))).astype(np.uint64)  # numpy %: the divisor's sign, as Python's
     return set_format(x, moduli, roots, True)
 
 

@@ -531,3 +531,73 @@ def test_mod_down_t_after_plain_same_objects(hip):
         out = torch.zeros((B, sq, n), dtype=torch.int64, device="cuda")
         H.approx_mod_down(pq, pp, down_bc, T["pinv_modq"], t, scaled.data_ptr(), out.data_ptr(), B, stream())
         assert np.array_equal(host(out), x), t
+
+
+def _centered_same_small(d, q, bound):
+    """[T][N] residues: every tower holds the same integer e with |e| < bound
+    (so the CRT value is e itself -- no big-integer lift needed)."""
+    qa = np.array(q, np.uint64)[:, None]
+    v = np.where(d > qa // np.uint64(2), d.astype(np.int64) - qa.astype(np.int64), d.astype(np.int64))
+    return bool(np.all(np.abs(v) < bound) and np.all(v == v[0:1]))
+
+
+@pytest.mark.parametrize("dnum", [1, 2, 3, 4])
+def test_configs4_digit_split_identities(hip, dnum):
+    """configs[4] shape (N = 2^17, Q = 48) at every digit split of
+    keyswitch-hybrid.cpp:341-346 for dnum = 1..4 (alpha = 48 / 24 / 16 / 12),
+    with P sized as OpenFHE sizes it for 60-bit towers (sizeP = alpha: P must
+    exceed every digit's modulus, rns-cryptoparameters.cpp:126-135), i.e.
+    P = 16 at the bench's dnum = 3:
+    (1) each digit j of EvalKeySwitchPrecomputeCore is ApproxModUp of c's
+        digit: on digit j's own towers it equals c, and
+        ApproxModDown(P * digit_j) returns digit_j's Q part exactly
+        (ApproxModDown of a multiple of P has a zero P part);
+    (2) KeySwitchCore with a zero key is zero;
+    (3) with keys built as KeySwitchGenInternal (keyswitch-hybrid.cpp:53-128)
+        from ternary s_old, s_new: ct0 + ct1 s_new - c s_old is one small
+        integer in all 48 towers.
+    These are the reference's own identities; the reference holds no
+    KeySwitchCore vector, so beyond them the key-switch oracle is parity
+    unpinned (DESIGN.md (c))."""
+    H, ctx = hip
+    import torch
+
+    log_n, sq = 17, 48
+    sp = (sq + dnum - 1) // dnum
+    n, q, rq, p, rp, kp, ks = _ks_case(H, ctx, log_n, sq, sp, dnum)
+    alpha, beta = ks.digits(sq)
+    assert (alpha, beta) == ((sq + dnum - 1) // dnum, dnum)
+    rng = np.random.default_rng(400 + dnum)
+    c = K.set_format(_uniform(rng, 1, q, n), q, rq, True)
+    dc = dev(c)
+    digits = torch.empty((1, beta, sq + sp, n), dtype=torch.int64, device="cuda")
+    ks.precompute(sq, dc.data_ptr(), digits.data_ptr(), 1, stream())
+    qp = H.NTTPlan(ctx, log_n, q + p, rq + rp)
+    Pm = 1
+    for x in p:
+        Pm *= x
+    for j in range(beta):
+        dj = digits[0, j].contiguous()
+        got_dj = host(dj)
+        st, en = j * alpha, min((j + 1) * alpha, sq)
+        assert np.array_equal(got_dj[st:en], c[0, st:en]), f"digit {j} keeps its own towers"
+        z = torch.empty_like(dj)
+        qp.mod_mul_scalar(dj.data_ptr(), [Pm % m for m in q + p], z.data_ptr(), 1, stream())
+        out = torch.empty((1, sq, n), dtype=torch.int64, device="cuda")
+        ks.mod_down(sq, z.data_ptr(), out.data_ptr(), 0, 1, stream())
+        assert np.array_equal(host(out)[0], got_dj[:sq]), f"ModDown(P * digit {j})"
+    zero = torch.zeros((dnum, sq + sp, n), dtype=torch.int64, device="cuda")
+    o0 = torch.empty((1, sq, n), dtype=torch.int64, device="cuda")
+    o1 = torch.empty_like(o0)
+    ks.core(sq, dc.data_ptr(), zero.data_ptr(), zero.data_ptr(), o0.data_ptr(), o1.data_ptr(), 0, 1, stream())
+    assert not host(o0).any() and not host(o1).any(), "zero key"
+    s_old, s_new = K.ternary(n, rng), K.ternary(n, rng)
+    kb, ka = K.keyswitch_gen(kp, s_old, s_new, rng)
+    dkb, dka = dev(kb), dev(ka)
+    ks.core(sq, dc.data_ptr(), dkb.data_ptr(), dka.data_ptr(), o0.data_ptr(), o1.data_ptr(), 0, 1, stream())
+    g0, g1 = host(o0), host(o1)
+    sn = K.small_poly_eval(s_new, q, rq)
+    so = K.small_poly_eval(s_old, q, rq)
+    lhs = O.eltwise("add", g0, O.eltwise("mul", g1, sn, q), q)
+    d = K.set_format(O.eltwise("sub", lhs, O.eltwise("mul", c, so, q), q), q, rq, False)
+    assert _centered_same_small(d[0], q, 1 << 40), "ct0 + ct1 s_new - c s_old is small"
