@@ -87,18 +87,36 @@ public:
     }
     void deallocate(void* p) { check(ofhe_hip_free_async(ctx_, p, nullptr), "HipManager::deallocate"); }
     void zero(void* dst, size_t bytes) { check(ofhe_hip_zero(ctx_, dst, bytes, nullptr), "HipManager::zero"); }
-    // Host <-> device copies of pageable memory are bracketed by stream syncs:
-    // HIP may stage them outside the stream's order, and the host buffer may
-    // be released as soon as the call returns.
+    // Host <-> device copies of the caller's (pageable) memory go through the
+    // manager's pinned staging buffer: one DMA from page-locked memory on the
+    // stream, in the stream's order, then a wait, so the caller's buffer and
+    // the staging buffer are free again when the call returns -- the
+    // synchronous copy_to_pim / copy_from_pim of PimManager.cpp:5-54.  No
+    // pageable hipMemcpyAsync: that path's staging and ordering are the HIP
+    // runtime's own (round 4's driver record read back stale words on it,
+    // DESIGN.md (c) "The round-4 adapter failure").
     void copy_to_device(void* dst, const void* src, size_t bytes) {
-        sync();
-        check(ofhe_hip_copy_to_device(ctx_, dst, src, bytes, nullptr), "HipManager::copy_to_device");
-        sync();
+        std::lock_guard<std::mutex> lk(stage_mu_);
+        sync();  // queued work that reads dst has finished
+        for (size_t off = 0; off < bytes;) {
+            const size_t n = std::min(bytes - off, stage_room(bytes - off));
+            std::memcpy(stage_, static_cast<const char*>(src) + off, n);
+            check(ofhe_hip_copy_to_device(ctx_, static_cast<char*>(dst) + off, stage_, n, nullptr),
+                  "HipManager::copy_to_device");
+            sync();  // the DMA has read the staging buffer
+            off += n;
+        }
     }
     void copy_from_device(void* dst, const void* src, size_t bytes) {
-        sync();
-        check(ofhe_hip_copy_to_host(ctx_, dst, src, bytes, nullptr), "HipManager::copy_from_device");
-        sync();
+        std::lock_guard<std::mutex> lk(stage_mu_);
+        for (size_t off = 0; off < bytes;) {
+            const size_t n = std::min(bytes - off, stage_room(bytes - off));
+            check(ofhe_hip_copy_to_host(ctx_, stage_, static_cast<const char*>(src) + off, n, nullptr),
+                  "HipManager::copy_from_device");
+            sync();  // queued producers, then the DMA, have finished
+            std::memcpy(static_cast<char*>(dst) + off, stage_, n);
+            off += n;
+        }
     }
     void sync() { check(ofhe_hip_sync(ctx_, nullptr), "HipManager::sync"); }
     // ofhe_hip_finalize refuses (OFHE_ERR_STATE) while DeviceBuffers still
@@ -106,6 +124,7 @@ public:
     // them (they free through the context handle, not through this object),
     // and process exit reclaims it.
     ~HipManager() {
+        if (stage_) (void)ofhe_hip_host_free(ctx_, stage_);
         if (ctx_) (void)ofhe_hip_finalize(ctx_);
     }
     HipManager(const HipManager&) = delete;
@@ -113,8 +132,27 @@ public:
 
 private:
     explicit HipManager(int device) : device_(device) { check(ofhe_hip_init(device, &ctx_), "HipManager"); }
+    // bytes the staging buffer takes per round (grown to the request, capped
+    // at kStageMax: larger copies go in rounds); caller holds stage_mu_
+    static constexpr size_t kStageMax = size_t(64) << 20;
+    size_t stage_room(size_t want) {
+        want = std::min(want, kStageMax);
+        if (stage_bytes_ < want) {
+            if (stage_) check(ofhe_hip_host_free(ctx_, stage_), "HipManager staging");
+            stage_ = nullptr;
+            stage_bytes_ = 0;
+            size_t b = 4096;
+            while (b < want) b <<= 1;
+            check(ofhe_hip_host_alloc(ctx_, b, &stage_), "HipManager staging");
+            stage_bytes_ = b;
+        }
+        return stage_bytes_;
+    }
     int device_;
     ofhe_ctx_t ctx_ = nullptr;
+    std::mutex stage_mu_;
+    void* stage_ = nullptr;
+    size_t stage_bytes_ = 0;
 };
 
 // RAII device buffer of uint64 words.
