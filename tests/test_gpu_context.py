@@ -47,3 +47,28 @@ def test_closed_context_rejects_use():
     ctx.close()  # idempotent on the Python side
     with pytest.raises(H.MathError):
         _ = ctx.handle
+
+
+def test_free_async_refuses_foreign_and_double_frees():
+    """ofhe_hip_free_async accepts only live ofhe_hip_alloc_async blocks of its
+    context: a hipMalloc'd pointer or a second free of the same block is an
+    argument error and leaves the live-block accounting (and so finalize's
+    refusal) intact (round-4 advisor finding)."""
+    import ofhe_hip as H
+
+    ctx = H.Context(0)
+    s = stream()
+    p = ctx.alloc_async(4096, s)
+    plain = ctx.alloc(4096)
+    with pytest.raises(H.MathError, match="not a live"):
+        ctx.free_async(plain, s)
+    ctx.free(plain)
+    ctx.free_async(p, s)
+    with pytest.raises(H.MathError, match="not a live"):
+        ctx.free_async(p, s)
+    q = ctx.alloc_async(64, s)
+    with pytest.raises(H.MathError, match="1 ofhe_hip_alloc_async"):
+        ctx.close()
+    ctx.free_async(q, s)
+    ctx.sync(s)
+    ctx.close()

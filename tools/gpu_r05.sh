@@ -6,6 +6,8 @@
 #   TESTS=1   the whole -m gpu suite (no -x: every failure is listed)
 #   BENCH=1   bench.py with BENCH_ARGS
 #   PROF=1    rocprofv3 kernel-trace stats of the bench
+#   OPRATE=1  tools/microbench/oprate4 (VALU issue cost in shader cycles)
+#   LISTPMC=1 the counters rocprofv3 offers on this device
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 TAG=${TAG:-r05}
@@ -26,6 +28,12 @@ if [ -n "$SOAK" ]; then
     for v in 0 1 2 3; do
         step copy_soak_v$v 120 tools/diag/copy_soak_bin $v ${SOAK_ITERS:-20000}
     done
+fi
+if [ -n "$OPRATE" ]; then
+    step oprate4 180 tools/microbench/oprate4_bin
+fi
+if [ -n "$LISTPMC" ]; then
+    step pmc_list 120 rocprofv3 --list-avail
 fi
 if [ -n "$TESTS" ]; then
     PYTHONUNBUFFERED=1 step pytest_gpu 600 python -u -m pytest tests -m gpu -q -rf --timeout 120 --timeout-method=thread ${PYTEST_ARGS}

@@ -7,6 +7,7 @@
 
 #include <atomic>
 #include <map>
+#include <set>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -131,7 +132,12 @@ struct ofhe_ctx_s {
     int device = 0;
     hipMemPool_t pool = nullptr;  // stream-ordered scratch + ofhe_hip_alloc_async (null: the default pool)
     std::atomic<int> live{1};
-    std::atomic<long> async_blocks{0};  // ofhe_hip_alloc_async blocks not yet freed (finalize refuses while > 0)
+    // ofhe_hip_alloc_async blocks not yet freed: finalize refuses while any
+    // is live.  A set, not a counter, so a pointer the pool never handed out
+    // (or one freed twice) cannot make the count wrong; the check and the
+    // teardown happen under the same lock as every insert / erase.
+    std::mutex blocks_mu;
+    std::set<void*> async_blocks;
 };
 
 enum { SPLIT_COLS = 0, SPLIT_T8 = 1, SPLIT_T9 = 2, SPLIT_T8B9 = 3 };

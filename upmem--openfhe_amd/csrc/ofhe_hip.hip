@@ -89,15 +89,18 @@ int ofhe_hip_trim(ofhe_ctx_t ctx, size_t keep_bytes) {
 
 int ofhe_hip_finalize(ofhe_ctx_t ctx) {
     if (!ctx) return fail(OFHE_ERR_ARG, "ctx is NULL");
-    if (ctx->live.load() == 0) return fail(OFHE_ERR_STATE, "context already finalized");
-    // Destroying the pool would release every block still allocated from it,
-    // leaving the caller's ofhe_hip_alloc_async pointers dangling: refuse, and
-    // keep the context usable, until all of them have been freed.
-    const long held = ctx->async_blocks.load();
-    if (held > 0)
-        return fail(OFHE_ERR_STATE, "ofhe_hip_finalize: " + std::to_string(held) +
-                                        " ofhe_hip_alloc_async block(s) still allocated; free them first");
-    if (ctx->live.exchange(0) == 0) return fail(OFHE_ERR_STATE, "context already finalized");
+    {
+        // Destroying the pool would release every block still allocated from
+        // it, leaving the caller's ofhe_hip_alloc_async pointers dangling:
+        // refuse, and keep the context usable, until all of them are freed.
+        std::lock_guard<std::mutex> lk(ctx->blocks_mu);
+        if (ctx->live.load() == 0) return fail(OFHE_ERR_STATE, "context already finalized");
+        const size_t held = ctx->async_blocks.size();
+        if (held > 0)
+            return fail(OFHE_ERR_STATE, "ofhe_hip_finalize: " + std::to_string(held) +
+                                            " ofhe_hip_alloc_async block(s) still allocated; free them first");
+        ctx->live.store(0);
+    }
     (void)hipSetDevice(ctx->device);
     (void)hipDeviceSynchronize();
     if (ctx->pool) (void)hipMemPoolDestroy(ctx->pool);  // only the library's own (freed) scratch is left in it
@@ -124,10 +127,12 @@ int ofhe_hip_free(ofhe_ctx_t ctx, void* dptr) {
 int ofhe_hip_alloc_async(ofhe_ctx_t ctx, size_t bytes, void** dptr, void* stream) {
     if (!ctx || !dptr) return fail(OFHE_ERR_ARG, "NULL argument");
     HIPCHK(hipSetDevice(ctx->device));
+    std::lock_guard<std::mutex> lk(ctx->blocks_mu);
+    if (ctx->live.load() == 0) return fail(OFHE_ERR_STATE, "context finalized");
     hipError_t e = ctx->pool ? hipMallocFromPoolAsync(dptr, bytes ? bytes : 1, ctx->pool, pick(stream))
                              : hipMallocAsync(dptr, bytes ? bytes : 1, pick(stream));
     if (e != hipSuccess) return fail(OFHE_ERR_NOMEM, std::string("hipMallocAsync: ") + hipGetErrorString(e));
-    ctx->async_blocks.fetch_add(1);
+    ctx->async_blocks.insert(*dptr);
     return OFHE_OK;
 }
 
@@ -135,8 +140,10 @@ int ofhe_hip_free_async(ofhe_ctx_t ctx, void* dptr, void* stream) {
     if (!ctx) return fail(OFHE_ERR_ARG, "ctx is NULL");
     if (!dptr) return OFHE_OK;
     HIPCHK(hipSetDevice(ctx->device));
+    std::lock_guard<std::mutex> lk(ctx->blocks_mu);
+    if (!ctx->async_blocks.erase(dptr))
+        return fail(OFHE_ERR_ARG, "ofhe_hip_free_async: not a live ofhe_hip_alloc_async block of this context");
     HIPCHK(hipFreeAsync(dptr, pick(stream)));
-    ctx->async_blocks.fetch_sub(1);
     return OFHE_OK;
 }
 
