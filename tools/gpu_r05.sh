@@ -8,6 +8,8 @@
 #   PROF=1    rocprofv3 kernel-trace stats of the bench
 #   OPRATE=1  tools/microbench/oprate4 (VALU issue cost in shader cycles)
 #   LISTPMC=1 the counters rocprofv3 offers on this device
+#   AB=1      same-process A/B of lib/variants/*.so (tools/exp_variants.py)
+#   PMCS=1    stall / issue counters of the pipeline kernels (tools/pmc_stall.sh)
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 TAG=${TAG:-r05}
@@ -37,6 +39,12 @@ if [ -n "$LISTPMC" ]; then
 fi
 if [ -n "$TESTS" ]; then
     PYTHONUNBUFFERED=1 step pytest_gpu 600 python -u -m pytest tests -m gpu -q -rf --timeout 120 --timeout-method=thread ${PYTEST_ARGS}
+fi
+if [ -n "$AB" ]; then
+    EXP_BATCH=${EXP_BATCH:-512} EXP_ROUNDS=${EXP_ROUNDS:-8} step exp_var 300 python -u tools/exp_variants.py
+fi
+if [ -n "$PMCS" ]; then
+    step pmc_stall 600 bash tools/pmc_stall.sh ${TAG}
 fi
 if [ -n "$BENCH" ]; then
     step bench 400 python -u bench.py ${BENCH_ARGS}

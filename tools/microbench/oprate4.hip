@@ -9,7 +9,8 @@
 // One workgroup per CU (grid = CUs), W waves per SIMD (blockDim = 256 W),
 // CH independent chains per thread, IT iterations.  Per SIMD the W waves
 // issue W * IT * CH instructions in (median wave elapsed) cycles.
-//   CH = 16, W = 1..4 -> throughput (cycles per wave64 instruction per SIMD)
+//   CH = 16, W = 1..4 -> throughput (cycles per wave64 instruction per SIMD);
+//   one 256 W-thread workgroup per CU, so W waves share each SIMD
 //   CH = 1,  W = 1    -> dependent-issue latency of one chain
 // Build: hipcc -O3 --offload-arch=gfx950 -o oprate4_bin oprate4.hip
 #include <hip/hip_runtime.h>
@@ -30,7 +31,7 @@
         __builtin_amdgcn_s_waitcnt(0);                                                              \
         const uint64_t t0 = __builtin_amdgcn_s_memtime();                                           \
         for (int i = 0; i < IT; i++) {                                                              \
-            _Pragma("unroll") for (int c = 0; c < CH; c++) asm volatile(ASM : "+v"(y[c]) : "v"(z)); \
+            _Pragma("unroll") for (int c = 0; c < CH; c++) asm volatile(ASM : "+v"(y[c]) : "v"(z) : "vcc"); \
         }                                                                                           \
         const uint64_t t1 = __builtin_amdgcn_s_memtime();                                           \
         uint32_t r = 0;                                                                             \
@@ -47,7 +48,7 @@
         __builtin_amdgcn_s_waitcnt(0);                                                              \
         const uint64_t t0 = __builtin_amdgcn_s_memtime();                                           \
         for (int i = 0; i < IT; i++) {                                                              \
-            _Pragma("unroll") for (int c = 0; c < CH; c++) asm volatile(ASM : "+v"(y[c]) : "v"(z)); \
+            _Pragma("unroll") for (int c = 0; c < CH; c++) asm volatile(ASM : "+v"(y[c]) : "v"(z) : "vcc"); \
         }                                                                                           \
         const uint64_t t1 = __builtin_amdgcn_s_memtime();                                           \
         uint64_t r = 0;                                                                             \
@@ -70,7 +71,7 @@ K32(k_addc_co, "v_addc_co_u32 %0, vcc, %0, %1, vcc")
 K32(k_cndmask, "v_cndmask_b32 %0, %0, %1, vcc")
 K32(k_fma_f32, "v_fma_f32 %0, %0, %1, %0")
 K32(k_mov_b32, "v_mov_b32 %0, %1")
-K64Z(k_mad_u64, uint32_t, "v_mad_u64_u32 %0, s[0:1], %1, %1, %0")
+K64Z(k_mad_u64, uint32_t, "v_mad_u64_u32 %0, vcc, %1, %1, %0")
 K64(k_lshl_add_u64, "v_lshl_add_u64 %0, %0, 0, %1")
 K64(k_cmp_u64, "v_cmp_le_u64 vcc, %0, %1")
 K64(k_lshr_b64, "v_lshrrev_b64 %0, 3, %0")
@@ -85,7 +86,12 @@ static double run(KFn kern, int ch, int waves, int ncu, uint64_t* dcyc, uint32_t
     double best = 1e30;
     for (int r = 0; r < reps; r++) {
         hipLaunchKernelGGL(kern, dim3(ncu), dim3(threads), 0, 0, dcyc, dout, 12345u + r);
-        (void)hipDeviceSynchronize();
+        hipError_t e = hipGetLastError();
+        if (e == hipSuccess) e = hipDeviceSynchronize();
+        if (e != hipSuccess) {
+            std::printf("launch failed: %s\n", hipGetErrorString(e));
+            std::exit(1);
+        }
         (void)hipMemcpy(c.data(), dcyc, nw * 8, hipMemcpyDeviceToHost);
         std::sort(c.begin(), c.end());
         const double med = (double)c[nw / 2];
@@ -115,24 +121,11 @@ int main() {
                 OP("v_lshl_add_u64", k_lshl_add_u64), OP("v_cmp_le_u64", k_cmp_u64), OP("v_lshrrev_b64", k_lshr_b64),
                 OP("v_fma_f64", k_fma_f64),         OP("v_mov_b64", k_mov_b64)};
     std::printf("# shader cycles per wave64 instruction per SIMD (s_memtime), %d CUs\n", ncu);
-    std::printf("%-18s %8s %8s %8s %8s %10s\n", "instruction", "W=1", "W=2", "W=4", "W=8", "latency");
+    std::printf("%-18s %8s %8s %8s %8s %10s\n", "instruction", "W=1", "W=2", "W=3", "W=4", "latency");
     for (auto& o : ops) {
         double t[4];
-        const int ws[4] = {1, 2, 4, 8};
-        for (int i = 0; i < 4; i++) {
-            // W = 8 needs 2048 threads per CU: two workgroups of 1024 per CU
-            if (ws[i] == 8) {
-                const int threads = 1024, nw = 2 * ncu * threads / 64;
-                std::vector<uint64_t> c(nw);
-                hipLaunchKernelGGL(o.thr, dim3(2 * ncu), dim3(threads), 0, 0, dcyc, dout, 777u);
-                (void)hipDeviceSynchronize();
-                (void)hipMemcpy(c.data(), dcyc, nw * 8, hipMemcpyDeviceToHost);
-                std::sort(c.begin(), c.end());
-                t[i] = (double)c[nw / 2] / ((double)IT * 16 * 8);
-            } else {
-                t[i] = run(o.thr, 16, ws[i], ncu, dcyc, dout);
-            }
-        }
+        const int ws[4] = {1, 2, 3, 4};
+        for (int i = 0; i < 4; i++) t[i] = run(o.thr, 16, ws[i], ncu, dcyc, dout);
         const double lat = run(o.lat, 1, 1, ncu, dcyc, dout);
         std::printf("%-18s %8.2f %8.2f %8.2f %8.2f %10.2f\n", o.name, t[0], t[1], t[2], t[3], lat);
     }

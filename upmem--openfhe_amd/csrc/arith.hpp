@@ -102,8 +102,16 @@ __device__ __forceinline__ u64 csub_s(u64 x, u64 m) {
 #ifndef OFHE_QH_ADDC
 #define OFHE_QH_ADDC 0  // measured: more instructions (add_co + cndmask), kept for reference
 #endif
+#ifndef OFHE_QH_MAD1
+#define OFHE_QH_MAD1 0  // 1: the quotient's second middle word added by a multiply-add by an opaque 1 (A/B: no gain)
+#endif
+// `one` is 1 held in an SGPR the compiler cannot see through (Mod::one, loaded
+// from the tower constants by the kernels' load_mod): then hi32(m2) * one + acc is ONE v_mad_u64_u32,
+// where the plain 64-bit add of two zero-extended words costs a v_mov_b32 (the
+// zero high word) plus a v_lshl_add_u64.  With a literal 1 LLVM folds the
+// multiply away and the add comes back.
 template <bool QA = false>
-__device__ __forceinline__ u64 mulhi_approx(u64 a, u64 b) {
+__device__ __forceinline__ u64 mulhi_approx(u64 a, u64 b, u32 one = 1) {
     if (QA) {
         // the two middle high words summed by add_co / addc_co straight into
         // an aligned (sum, carry) pair: the 64-bit accumulator of the final
@@ -131,6 +139,7 @@ __device__ __forceinline__ u64 mulhi_approx(u64 a, u64 b) {
     }
     const u64 m1 = mad32(lo32(a), hi32(b), 0);
     const u64 m2 = mad32(hi32(a), lo32(b), 0);
+    if (OFHE_QH_MAD1) return mad32(hi32(m2), one, mad32(hi32(a), hi32(b), m1 >> 32));
     return mad32(hi32(a), hi32(b), (m1 >> 32) + (m2 >> 32));
 }
 
@@ -161,6 +170,7 @@ struct Mod {
     u64 nq4;  // 2^64 - 4q
     u64 nq8;  // 2^64 - 8q
     u32 sh;   // L - 32 (SPQ only)
+    u32 one = 1;  // 1; loaded from TowerConst (opaque to LLVM) in the NTT kernels, see mulhi_approx
 };
 
 // Shoup with precomputed wp = floor(w*2^64/q): a*w mod q in [0, 4q) for any
@@ -169,7 +179,7 @@ struct Mod {
 // lo64(a*w) + lo64(qh*(2^64-q)), so there is no 64-bit subtraction.
 template <bool SPQ, bool QA>
 __device__ __forceinline__ u64 shoup_lazy(u64 a, u64 w, u64 wp, const Mod<SPQ, QA>& M) {
-    const u64 qh = mulhi_approx<QA>(a, wp);
+    const u64 qh = mulhi_approx<QA>(a, wp, M.one);
     u64 s = mad32(lo32(a), lo32(w), 0);
     s = mad32(lo32(qh), lo32(M.nq), s);
     u32 hi;
@@ -189,7 +199,7 @@ __device__ __forceinline__ u64 shoup_lazy(u64 a, u64 w, u64 wp, const Mod<SPQ, Q
 // call site, so the wrap-around arithmetic returns it exactly).
 template <bool SPQ, bool QA>
 __device__ __forceinline__ u64 shoup_lazy_acc(u64 a, u64 w, u64 wp, const Mod<SPQ, QA>& M, u64 acc) {
-    const u64 qh = mulhi_approx<QA>(a, wp);
+    const u64 qh = mulhi_approx<QA>(a, wp, M.one);
     u64 s = mad32(lo32(a), lo32(w), acc);
 #if OFHE_ACC_PIN
     asm("" : "+v"(s));  // keeps LLVM from re-associating acc out of the mad chain

@@ -46,6 +46,8 @@ struct TowerConst {
     u32 nshift;    // msb(q) - 2
     u32 spq_sh;    // msb(q) - 32 when q = 2^msb - d with d < 2^32, else 0
     u64 qinv;      // q^-1 mod 2^64 (Montgomery Hadamard)
+    u32 one;       // 1, loaded so LLVM cannot fold it (Mod::one, mulhi_approx)
+    u32 pad_;
 };
 // Shoup quotient form per kernel (Mod<SPQ, QA>, arith.hpp): add_co/addc into
 // the accumulator pair (1) or zero-extending moves and a 64-bit add (0).
@@ -70,7 +72,7 @@ struct TowerConst {
 #endif
 template <bool SPQ, bool QA = false>
 __device__ __forceinline__ Mod<SPQ, QA> load_mod(const TowerConst& tc) {
-    return Mod<SPQ, QA>{tc.q, 4 * tc.q, 8 * tc.q, tc.nq, tc.nq4, 0 - 8 * tc.q, tc.spq_sh};
+    return Mod<SPQ, QA>{tc.q, 4 * tc.q, 8 * tc.q, tc.nq, tc.nq4, 0 - 8 * tc.q, tc.spq_sh, tc.one};
 }
 
 // Device view of a plan. Twiddles are interleaved (w, w') pairs so one

@@ -343,6 +343,7 @@ int ofhe_hip_plan_create_ex(ofhe_ctx_t ctx, uint32_t log_n, uint32_t towers, con
         c.spq_sh = spq ? mb - 32 : 0;
         c.nq = 0 - qt;
         c.nq4 = 0 - 4 * qt;
+        c.one = 1;
         u64 inv = qt;  // q^-1 mod 2^64 by Newton iteration (q odd)
         for (int it = 0; it < 6; it++) inv *= 2 - qt * inv;
         c.qinv = inv;
