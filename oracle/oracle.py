@@ -64,6 +64,7 @@ def lib() -> ctypes.CDLL:
                                                       _u64p, _u64p, _u64p, _u64p, _u64p, _u64p]),
             "oracle_base_conv_precompute": (None, [ctypes.c_uint, ctypes.c_uint, _u64p, _u64p, _u64p, _u64p,
                                                    _u64p, _u64p, _u64p]),
+            "oracle_automorphism": (None, [_u64p, _u64p, _u64, ctypes.c_uint32, ctypes.c_int, _u64]),
             "oracle_splitmix64": (_u64, [_u64p]),
             "oracle_fill_uniform": (None, [_u64p, _u64, _u64, _u64p]),
             "oracle_fnv64": (_u64, [_u64p, _u64]),

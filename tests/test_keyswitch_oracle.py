@@ -192,3 +192,25 @@ def test_automorphism_reference_kat():
     ev = O.ntt_fwd(np.array(t["x"], np.uint64).reshape(1, 1, 4), tb).reshape(-1)
     back = O.ntt_inv(K.automorphism(ev, t["k"], True, k["q"]).reshape(1, 1, 4), tb).reshape(-1)
     assert back.tolist() == t["expected"]
+
+
+@pytest.mark.parametrize("log_n", [2, 5, 10])
+@pytest.mark.parametrize("eval_form", [False, True])
+def test_c_oracle_automorphism_equals_python(log_n, eval_form):
+    """oracle_automorphism (C, used by tests/cpp/test_hooks.cpp) equals the
+    Python restatement of PolyImpl::AutomorphismTransform (poly-impl.h:312-365)
+    for every odd k below 2N, zeros included (a negated zero stays q)."""
+    import ctypes
+
+    n = 1 << log_n
+    q, _ = O.moduli_chain(max(log_n, 2), 1)
+    q = q[0]
+    rng = np.random.default_rng(log_n)
+    x = rng.integers(0, q, size=n, dtype=np.uint64)
+    x[::3] = 0
+    L = O.lib()
+    for k in range(1, 2 * n, 2):
+        out = np.zeros(n, np.uint64)
+        L.oracle_automorphism(x.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)),
+                              out.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)), n, k, int(eval_form), q)
+        assert np.array_equal(out, K.automorphism(x, k, eval_form, q)), k
