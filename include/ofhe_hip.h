@@ -121,11 +121,6 @@ typedef struct ofhe_plan_options {
     uint32_t split;          /* OFHE_SPLIT_*; log_n <= 12 plans accept only AUTO          */
     uint32_t generic_moduli; /* 1: the generic-modulus kernels even when every q is a
                                 special prime 2^L - d (the default picks the faster ones) */
-    uint32_t cached_intermediates; /* 1: ofhe_hip_ntt_mul_intt at log_n = 16 (8 | 8 split)
-                                passes its intermediates between the three launches
-                                through the caches instead of streaming them past,
-                                for chunked runs (ofhe_hip_plan_tune) whose chunk fits
-                                the Infinity Cache                                     */
 } ofhe_plan_options;
 int ofhe_hip_plan_create_ex(ofhe_ctx_t ctx, uint32_t log_n, uint32_t towers, const uint64_t* q,
                             const uint64_t* psi, const ofhe_plan_options* options, ofhe_plan_t* plan);

@@ -10,7 +10,6 @@
 #   LISTPMC=1 the counters rocprofv3 offers on this device
 #   AB=1      same-process A/B of lib/variants/*.so (tools/exp_variants.py)
 #   PMCS=1    stall / issue counters of the pipeline kernels (tools/pmc_stall.sh)
-#   CHUNK=1   chunked pipeline A/B, streamed vs cached intermediates (tools/exp_chunk.py)
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 TAG=${TAG:-r05}
@@ -43,9 +42,6 @@ if [ -n "$TESTS" ]; then
 fi
 if [ -n "$AB" ]; then
     EXP_BATCH=${EXP_BATCH:-512} EXP_ROUNDS=${EXP_ROUNDS:-8} step exp_var 300 python -u tools/exp_variants.py
-fi
-if [ -n "$CHUNK" ]; then
-    step exp_chunk 400 python -u tools/exp_chunk.py
 fi
 if [ -n "$PMCS" ]; then
     step pmc_stall 600 bash tools/pmc_stall.sh ${TAG}

@@ -802,15 +802,12 @@ __device__ __forceinline__ void block_body(const PlanArgs& P, const u64* src, u6
 #pragma unroll
     for (int k = 0; k < 16; k++) st_m<NTO>(oblk + tid + 256 * k, v[k]);
 }
-// IM (block_body): 0 streams the polynomial data (non-temporal); the chunked
-// pipeline with cached intermediates (ofhe_plan_options.cached_intermediates)
-// uses 3: the column pass's output read and the inverse input written cached
-template <int MODE, bool SPQ, int NR, int SK = 0, int IM = 0>
+template <int MODE, bool SPQ, int NR, int SK = 0>
 __global__ __launch_bounds__(256, OFHE_KB_WAVES) void k_block(PlanArgs P, const u64* src, u64* dst,
                                                               const u64* __restrict__ bdat, u32 batch, u32 nwg) {
     OFHE_VGPR_FLOOR();
     __shared__ u64 lds[LDS_WORDS];
-    block_body<MODE, SPQ, NR, SK, IM>(P, src, dst, bdat, batch, xcd_remap(blockIdx.x, nwg), lds, threadIdx.x);
+    block_body<MODE, SPQ, NR, SK>(P, src, dst, bdat, batch, xcd_remap(blockIdx.x, nwg), lds, threadIdx.x);
 }
 
 // Rescaling source of the forward column pass (k_cols / k_tcols <.., SWS = true>):
@@ -980,14 +977,12 @@ __device__ __forceinline__ void tcols_body(const PlanArgs& P, const u64* src, u6
     }
 }
 
-// IM as k_block's: 2 (forward: output cached) / 1 (inverse: input cached) in
-// the chunked pipeline with cached intermediates
-template <bool INV, bool SPQ, bool SWS = false, int LOGN = 16, int IM = 0>
+template <bool INV, bool SPQ, bool SWS = false, int LOGN = 16>
 __global__ __launch_bounds__(16 * TCOLS_W, (INV && OFHE_TCOLS_HALF) ? OFHE_TCOLS_HALF_WAVES : OFHE_KB_WAVES) void k_tcols(
     PlanArgs P, const u64* src, u64* dst, u32 batch, u32 nwg, SwSrc SWA) {
     OFHE_VGPR_FLOOR();
     __shared__ u64 lds[INV ? TCOLS_LDS_INV_WORDS : TCOLS_LDS_WORDS];
-    tcols_body<INV, SPQ, SWS, LOGN, IM>(P, src, dst, batch, xcd_remap(blockIdx.x, nwg), SWA, lds, threadIdx.x);
+    tcols_body<INV, SPQ, SWS, LOGN>(P, src, dst, batch, xcd_remap(blockIdx.x, nwg), SWA, lds, threadIdx.x);
 }
 
 // ---------------------------------------------------------------------------

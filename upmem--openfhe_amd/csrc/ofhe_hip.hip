@@ -209,7 +209,6 @@ int ofhe_hip_plan_create_ex(ofhe_ctx_t ctx, uint32_t log_n, uint32_t towers, con
     if (towers < 1 || towers > 4096) return fail(OFHE_ERR_ARG, "towers must be in [1, 4096]");
     const ofhe_plan_options opt = options ? *options : ofhe_plan_options{};
     if (opt.generic_moduli > 1) return fail(OFHE_ERR_ARG, "options.generic_moduli must be 0 or 1");
-    if (opt.cached_intermediates > 1) return fail(OFHE_ERR_ARG, "options.cached_intermediates must be 0 or 1");
     // Pass split for log_n > 12 (DESIGN.md "Why not a 10 | 6 split" and the
     // rejected-variant table): 8 | 8 at N = 2^16 (k_tcols + an 8-stage block
     // pass), k_cols + the 12-stage block pass elsewhere; the other splits are
@@ -540,28 +539,19 @@ static void launch_cols(const PlanArgs& a, bool spq, bool inv, const u64* src, u
         launch_cols_s<false>(a, inv, src, dst, batch, s);
 }
 
-// column pass for log_n > 12: k_tcols / k_tcols9 (8 / 9 stages) unless SPLIT_COLS, else k_cols;
-// cached: the chunked pipeline's cached intermediates (SPLIT_T8 only)
+// column pass for log_n > 12: k_tcols / k_tcols9 (8 / 9 stages) unless SPLIT_COLS, else k_cols
 static void launch_colpass(const PlanArgs& a, bool spq, int split, bool inv, const u64* src, u64* dst, u32 batch,
-                           hipStream_t s, bool cached = false);
+                           hipStream_t s);
 
 // Pass split for log_n > 12 (the plan's split, internal.hpp): the block pass
 // runs the last 8 (SPLIT_T8 / T9: k_block NR = 2), 9 (SPLIT_T8B9: NR = 3
 // without the first three stages of its first round) or 12 stages.
 template <int MODE>
 static void launch_block(const PlanArgs& a, bool spq, const u64* src, u64* dst, const u64* b, u32 batch,
-                         hipStream_t s, int split = SPLIT_COLS, bool cached = false) {
+                         hipStream_t s, int split = SPLIT_COLS) {
     const u32 nwg = batch * a.towers * (1u << (a.log_n - 12));
 #define LB(SP, NR, SK) \
     hipLaunchKernelGGL((k_block<MODE, SP, NR, SK>), dim3(nwg), dim3(256), 0, s, a, src, dst, b, batch, nwg)
-    if (MODE == MODE_FUSED && cached && split == SPLIT_T8) {
-        // chunked pipeline, cached intermediates (ofhe_plan_options.cached_intermediates)
-        if (spq)
-            hipLaunchKernelGGL((k_block<MODE, true, 2, 0, 3>), dim3(nwg), dim3(256), 0, s, a, src, dst, b, batch, nwg);
-        else
-            hipLaunchKernelGGL((k_block<MODE, false, 2, 0, 3>), dim3(nwg), dim3(256), 0, s, a, src, dst, b, batch, nwg);
-        return;
-    }
     if (split == SPLIT_T8 || split == SPLIT_T9) {
         if (spq) LB(true, 2, 0); else LB(false, 2, 0);
     } else if (split == SPLIT_T8B9) {
@@ -573,7 +563,7 @@ static void launch_block(const PlanArgs& a, bool spq, const u64* src, u64* dst, 
 }
 
 static void launch_tcols(const PlanArgs& a, bool spq, int split, bool inv, const u64* src, u64* dst, u32 batch,
-                         hipStream_t s, bool cached = false) {
+                         hipStream_t s) {
     if (split == SPLIT_T8B9) {
         const u32 nwg = batch * a.towers * (512 / TCOLS_W);
 #define LT17(I, SP)                                                                                           \
@@ -599,20 +589,6 @@ static void launch_tcols(const PlanArgs& a, bool spq, int split, bool inv, const
         return;
     }
     const u32 nwg = batch * a.towers * (256 / TCOLS_W);
-    if (cached) {
-        // chunked pipeline, cached intermediates: the forward pass stores, the
-        // inverse pass loads, through the caches (IM 2 / 1, k_tcols)
-#define LTC(I, SP, IM)                                                                                         \
-    hipLaunchKernelGGL((k_tcols<I, SP, false, 16, IM>), dim3(nwg), dim3(16 * TCOLS_W), 0, s, a, src, dst, batch, nwg, \
-                       SwSrc{nullptr, 0, 0, nullptr, 1, 0})
-        if (inv) {
-            if (spq) LTC(true, true, 1); else LTC(true, false, 1);
-        } else {
-            if (spq) LTC(false, true, 2); else LTC(false, false, 2);
-        }
-#undef LTC
-        return;
-    }
 #define LT(I, SP)                                                                                 \
     hipLaunchKernelGGL((k_tcols<I, SP>), dim3(nwg), dim3(16 * TCOLS_W), 0, s, a, src, dst, batch, nwg, \
                        SwSrc{nullptr, 0, 0, nullptr, 1, 0})
@@ -636,9 +612,9 @@ static void launch_small(const PlanArgs& a, bool spq, const u64* src, u64* dst, 
 }
 
 static void launch_colpass(const PlanArgs& a, bool spq, int split, bool inv, const u64* src, u64* dst, u32 batch,
-                           hipStream_t s, bool cached) {
+                           hipStream_t s) {
     if (split != SPLIT_COLS)
-        launch_tcols(a, spq, split, inv, src, dst, batch, s, cached && split == SPLIT_T8);
+        launch_tcols(a, spq, split, inv, src, dst, batch, s);
     else
         launch_cols(a, spq, inv, src, dst, batch, s);
 }
@@ -832,10 +808,9 @@ int ofhe_hip_ntt_mul_intt(ofhe_plan_t p, const uint64_t* a_, const uint64_t* b, 
             const u32 n = batch - b0 < cb ? batch - b0 : cb;
             hipStream_t sx = multi ? p->st[idx & 1] : s;
             const u64 off = (u64)b0 * words;
-            const bool ci = p->opts.cached_intermediates != 0;
-            launch_colpass(a, p->spq, p->split, false, a_ + off, c + off, n, sx, ci);
-            launch_block<MODE_FUSED>(a, p->spq, c + off, c + off, b + off, n, sx, p->split, ci);
-            launch_colpass(a, p->spq, p->split, true, c + off, c + off, n, sx, ci);
+            launch_colpass(a, p->spq, p->split, false, a_ + off, c + off, n, sx);
+            launch_block<MODE_FUSED>(a, p->spq, c + off, c + off, b + off, n, sx, p->split);
+            launch_colpass(a, p->spq, p->split, true, c + off, c + off, n, sx);
         }
         if (multi) {
             for (int i = 0; i < 2; i++) {

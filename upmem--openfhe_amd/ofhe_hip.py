@@ -175,8 +175,7 @@ BCONV_KERNEL_AUTO, BCONV_KERNEL_LIMB, BCONV_KERNEL_WIDE = range(3)
 
 
 class PlanOptions(ctypes.Structure):
-    _fields_ = [("split", ctypes.c_uint32), ("generic_moduli", ctypes.c_uint32),
-                ("cached_intermediates", ctypes.c_uint32)]
+    _fields_ = [("split", ctypes.c_uint32), ("generic_moduli", ctypes.c_uint32)]
 
 
 class BconvOptions(ctypes.Structure):
@@ -270,7 +269,7 @@ class NTTPlan:
     """
 
     def __init__(self, ctx: Context, log_n: int, moduli: Sequence[int], roots: Sequence[int],
-                 split: int = SPLIT_AUTO, generic_moduli: bool = False, cached_intermediates: bool = False):
+                 split: int = SPLIT_AUTO, generic_moduli: bool = False):
         if len(moduli) != len(roots):
             raise MathError("moduli and roots differ in length")
         self.ctx = ctx
@@ -280,7 +279,7 @@ class NTTPlan:
         self.roots = [int(r) for r in roots]
         self.towers = len(self.moduli)
         h = _vp()
-        o = PlanOptions(int(split), 1 if generic_moduli else 0, 1 if cached_intermediates else 0)
+        o = PlanOptions(int(split), 1 if generic_moduli else 0)
         _check(lib().ofhe_hip_plan_create_ex(ctx.handle, self.log_n, self.towers, _arr(self.moduli),
                                              _arr(self.roots), _opt_ptr(o), ctypes.byref(h)))
         self._h = h
