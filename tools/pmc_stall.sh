@@ -4,15 +4,23 @@
 # kernel-trace-only rocprofv3 run of the headline configuration (<= 8 SQ
 # counters per pass, MI355X_MICROARCH.md §HBM/rocprofv3).  Usage:
 #   tools/pmc_stall.sh <tag>  -> gpurun_out/pmcs_<tag>/ and gpurun_out/pmcs_<tag>.json
+# STALL_OP=fwd|inv profiles the standalone transforms instead (tools/run_pipeline.py,
+# configs[2] shape, RUN_BATCH / RUN_REPS from the environment).
 R="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 TAG="${1:-current}"
 OUT="$R/gpurun_out/pmcs_$TAG"
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
+if [ -n "$STALL_OP" ]; then
+  export RUN_OP="$STALL_OP" RUN_BATCH="${RUN_BATCH:-1024}" RUN_REPS="${RUN_REPS:-3}"
+  CMD=("$R/tools/run_pipeline.py")
+else
+  CMD=("$R/bench.py" --steps 2 --warmup 1 --no-extras --no-check ${PMC_ARGS})
+fi
 pass() {  # name, counters...
   local name="$1"; shift
   timeout -s KILL ${PMC_TIMEOUT:-240} rocprofv3 --pmc "$@" --kernel-trace --output-format csv -d "$OUT/$name" -o run \
-      -- python3 "$R/bench.py" --steps 2 --warmup 1 --no-extras --no-check ${PMC_ARGS} \
+      -- python3 "${CMD[@]}" \
       > "$OUT/$name.stdout" 2> "$OUT/$name.err" || { echo "pmc pass $name failed rc=$?"; tail -5 "$OUT/$name.err"; exit 1; }
   echo "pmc pass $name done"
 }

@@ -17,7 +17,7 @@ import os
 import sys
 
 d = sys.argv[1]
-NAMES = {"k_block<2,": "k_block<fused>", "k_tcols<false": "colpass<fwd>", "k_tcols<true": "colpass<inv>"}
+NAMES = {"k_block<2,": "k_block<fused>", "k_block<0,": "k_block<fwd>", "k_block<1,": "k_block<inv>", "k_tcols<false": "colpass<fwd>", "k_tcols<true": "colpass<inv>"}
 
 
 def kname(n):
