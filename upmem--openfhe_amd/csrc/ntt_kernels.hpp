@@ -122,22 +122,6 @@ __device__ __forceinline__ void st_s(u64* p, u64 v) {
     else
         *p = v;
 }
-// streaming (NT = true, as ld_s / st_s) or cached access, chosen per call site;
-// ld_m<LD_SC1> loads with sc1 (served by the XCD's L2, bypassing the CU's L1:
-// data another CU of the same XCD stored in the same launch)
-enum { LD_PLAIN = 0, LD_NT = 1, LD_SC1 = 2 };
-template <int LD>
-__device__ __forceinline__ u64 ld_m(const u64* p) {
-    if (LD == LD_SC1) return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    return LD == LD_NT ? ld_s(p) : *p;
-}
-template <bool NT>
-__device__ __forceinline__ void st_m(u64* p, u64 v) {
-    if (NT)
-        st_s(p, v);
-    else
-        *p = v;
-}
 __device__ __forceinline__ u64x2 ld2_s(const u64* p) {
     const u64x2* q = reinterpret_cast<const u64x2*>(p);
     return OFHE_NT ? __builtin_nontemporal_load(q) : *q;
@@ -612,19 +596,12 @@ __device__ __forceinline__ void wave_stage_out(const u64 (&v)[16], u64* lds, u32
 // its last stage (stride 256) and the inverse round 1' its first (t = 256);
 // the inverse twist is the one of 512-element groups.
 // The body of k_block for work item wid (block g = wid % G of polynomial
-// tower pb = wid / G), on the caller's LDS (LDS_WORDS words).  IM: bit 0 =
-// the input is an intermediate another pass of the same launch wrote (cached
-// loads), bit 1 = the output is one (cached stores), bit 2 = load that input
-// with sc1 (L1 bypass, no acquire needed) -- for a pass fed by another pass
-// of the same launch (round 4's persistent pipeline, removed in round 5);
-// 0 streams both.
-template <int MODE, bool SPQ, int NR, int SK = 0, int IM = 0>
+// tower pb = wid / G), on the caller's LDS (LDS_WORDS words).
+template <int MODE, bool SPQ, int NR, int SK = 0>
 __device__ __forceinline__ void block_body(const PlanArgs& P, const u64* src, u64* dst, const u64* __restrict__ bdat,
                                            u32 batch, u32 wid, u64* lds, u32 tid) {
     static_assert(NR == 2 || NR == 3, "k_block covers the last 8 (NR=2) or 12 (NR=3) stages");
     static_assert(SK == 0 || (SK == 3 && NR == 3), "k_block: SK = 3 needs NR = 3");
-    constexpr int LDI = (IM & 4) ? LD_SC1 : ((IM & 1) ? LD_PLAIN : LD_NT);
-    constexpr bool NTO = !(IM & 2);
     const u32 logn = P.log_n;
     const u32 N = 1u << logn;
     const u32 G = N >> 12;  // blocks per polynomial
@@ -651,7 +628,7 @@ __device__ __forceinline__ void block_body(const PlanArgs& P, const u64* src, u6
         if (NR == 3) {
             // round 1: st = 256, p = tid + 256k
 #pragma unroll
-            for (int k = 0; k < 16; k++) v[k] = ld_m<LDI>(blk + tid + 256 * k);
+            for (int k = 0; k < 16; k++) v[k] = ld_s(blk + tid + 256 * k);
             if (SK == 3)
                 fwd_stage16<3>(v, tw, (N >> 12) + g, M);  // input < 12q (k_tcols) -> < 12q
             else
@@ -664,7 +641,7 @@ __device__ __forceinline__ void block_body(const PlanArgs& P, const u64* src, u6
             for (int k = 0; k < 16; k++) v[k] = lds[L2 + 17 * k];
         } else {
 #pragma unroll
-            for (int k = 0; k < 16; k++) v[k] = ld_m<LDI>(blk + h * 256 + r + 16 * k);
+            for (int k = 0; k < 16; k++) v[k] = ld_s(blk + h * 256 + r + 16 * k);
         }
         fwd_round16(v, tw, (N >> 8) + g * 16 + h, M);
 #pragma unroll
@@ -781,7 +758,7 @@ __device__ __forceinline__ void block_body(const PlanArgs& P, const u64* src, u6
         for (int k = 0; k < 16; k++) {
             const u32 p = h * 256 + r + 16 * k;
             const Tw f = ldtw(tw_, p);
-            st_m<NTO>(oblk + p, shoup_lazy(v[k], f.w, f.wp, M));
+            st_s(oblk + p, shoup_lazy(v[k], f.w, f.wp, M));
         }
         return;
     }
@@ -800,7 +777,7 @@ __device__ __forceinline__ void block_body(const PlanArgs& P, const u64* src, u6
         v[k] = logn == 12 ? twist_out(v[k], f, M) : shoup_lazy(v[k], f.w, f.wp, M);
     }
 #pragma unroll
-    for (int k = 0; k < 16; k++) st_m<NTO>(oblk + tid + 256 * k, v[k]);
+    for (int k = 0; k < 16; k++) st_s(oblk + tid + 256 * k, v[k]);
 }
 template <int MODE, bool SPQ, int NR, int SK = 0>
 __global__ __launch_bounds__(256, OFHE_KB_WAVES) void k_block(PlanArgs P, const u64* src, u64* dst,
@@ -855,14 +832,11 @@ constexpr u32 TCOLS_LDS_WORDS = 16 * 16 * TCOLS_W + 16 * 16;
 #endif
 constexpr u32 TCOLS_LDS_INV_WORDS = OFHE_TCOLS_HALF ? 8 * 16 * TCOLS_W : TCOLS_LDS_WORDS;
 // The body of k_tcols for work item wid (column tile cb = wid % (S / W) of
-// polynomial tower pb = wid / (S / W)) on the caller's LDS (TCOLS_LDS_WORDS);
-// IM as block_body's.
-template <bool INV, bool SPQ, bool SWS = false, int LOGN = 16, int IM = 0>
+// polynomial tower pb = wid / (S / W)) on the caller's LDS (TCOLS_LDS_WORDS).
+template <bool INV, bool SPQ, bool SWS = false, int LOGN = 16>
 __device__ __forceinline__ void tcols_body(const PlanArgs& P, const u64* src, u64* dst, u32 batch, u32 wid,
                                            const SwSrc& SWA, u64* lds, u32 tid) {
     static_assert(LOGN == 16 || LOGN == 17, "k_tcols: N = 2^16 or 2^17");
-    constexpr int LDI = (IM & 4) ? LD_SC1 : ((IM & 1) ? LD_PLAIN : LD_NT);
-    constexpr bool NTO = !(IM & 2);
     constexpr u32 N = 1u << LOGN, S = N / 256, W = TCOLS_W;
     // Exchange patterns p = tid + 16W k (round 1) and p = 16W h + W k + r
     // (round 2).  The inverse writes the second and reads the first: unpadded,
@@ -900,7 +874,7 @@ __device__ __forceinline__ void tcols_body(const PlanArgs& P, const u64* src, u6
             }
         } else {
 #pragma unroll
-            for (int k = 0; k < 16; k++) v[k] = ld_m<LDI>(x + (u64)(h + 16 * k) * S + r);
+            for (int k = 0; k < 16; k++) v[k] = ld_s(x + (u64)(h + 16 * k) * S + r);
         }
         fwd_round16_canon(v, tw, 1, M);
 #pragma unroll
@@ -911,11 +885,11 @@ __device__ __forceinline__ void tcols_body(const PlanArgs& P, const u64* src, u6
         for (int k = 0; k < 16; k++) v[k] = lds[h * RP + r + W * k];
         fwd_round16(v, tw, 16 + h, M);
 #pragma unroll
-        for (int k = 0; k < 16; k++) st_m<NTO>(y + (u64)(16 * h + k) * S + r, v[k]);
+        for (int k = 0; k < 16; k++) st_s(y + (u64)(16 * h + k) * S + r, v[k]);
     } else {
         const u64* itw = P.itw + (u64)t * N * 2;
 #pragma unroll
-        for (int k = 0; k < 16; k++) v[k] = ld_m<LDI>(x + (u64)(16 * h + k) * S + r);
+        for (int k = 0; k < 16; k++) v[k] = ld_s(x + (u64)(16 * h + k) * S + r);
         if (OFHE_LAZY_GS) {
             // input < 4q (the block pass's lazy twist); round 2's registers all
             // come from one round-1 position, taken as < 8q
@@ -962,7 +936,7 @@ __device__ __forceinline__ void tcols_body(const PlanArgs& P, const u64* src, u6
             inv_round16_b(v, b8, itw, 1, M);
 #pragma unroll
             for (int k = 0; k < 16; k++)
-                st_m<NTO>(y + (u64)(h + 16 * k) * S + r, b8[k] ? canon8m(v[k], M) : canon4m(v[k], M));
+                st_s(y + (u64)(h + 16 * k) * S + r, b8[k] ? canon8m(v[k], M) : canon4m(v[k], M));
         } else {
             inv_round16(v, itw, 16 + h, M);
 #pragma unroll
@@ -972,7 +946,7 @@ __device__ __forceinline__ void tcols_body(const PlanArgs& P, const u64* src, u6
             for (int k = 0; k < 16; k++) v[k] = lds[L1 + 16 * W * k];
             inv_round16(v, itw, 1, M);
 #pragma unroll
-            for (int k = 0; k < 16; k++) st_m<NTO>(y + (u64)(h + 16 * k) * S + r, canon4m(v[k], M));
+            for (int k = 0; k < 16; k++) st_s(y + (u64)(h + 16 * k) * S + r, canon4m(v[k], M));
         }
     }
 }
