@@ -5,6 +5,8 @@ Mirrors the reference's own tests: UnitTestTransform (KAT), UnitTestNTT
 (round trips), UnitTestMubintvec (vector ModAdd/ModSub/ModMul KATs),
 UnitTestDCRTElements (random DCRTPoly + and * against an independent check).
 """
+import ctypes
+
 import numpy as np
 import pytest
 from conftest import load_golden
@@ -444,6 +446,41 @@ def test_errors_raise(hip, O):
         plan.forward(0, 1, stream())                   # NULL data
     with pytest.raises(H.MathError):
         plan.forward(1 << 20, 0, stream())             # empty batch
+
+
+def test_creation_options_refused(hip, O):
+    """Creation options outside their domain are refused with OFHE_ERR_ARG
+    (ofhe_hip_plan_create_ex / _bconv_create_ex / _ks_create_ex), never
+    silently replaced by a default kernel: every split names the log_n it
+    applies to, and flags are 0 or 1."""
+    H, ctx = hip
+    bad_splits = [(10, H.SPLIT_COLS), (10, H.SPLIT_8_8), (17, H.SPLIT_8_8), (16, H.SPLIT_9_8),
+                  (16, H.SPLIT_8_9), (14, H.SPLIT_8_9), (16, 5), (17, 99)]
+    for log_n, split in bad_splits:
+        qs, rs = O.moduli_chain(log_n, 1)
+        with pytest.raises(H.MathError):
+            H.NTTPlan(ctx, log_n, qs, rs, split=split)
+    qs, rs = O.moduli_chain(16, 1)
+    o = H.PlanOptions(H.SPLIT_AUTO, 2)                  # generic_moduli is a flag
+    h = H._vp()
+    assert H.lib().ofhe_hip_plan_create_ex(ctx.handle, 16, 1, H._arr(qs), H._arr(rs), H._opt_ptr(o),
+                                           ctypes.byref(h)) != 0
+    for log_n, split in ((13, H.SPLIT_COLS), (16, H.SPLIT_8_8), (17, H.SPLIT_9_8), (17, H.SPLIT_8_9)):
+        qs, rs = O.moduli_chain(log_n, 1)
+        H.NTTPlan(ctx, log_n, qs, rs, split=split).close()  # the accepted combinations
+    q, _ = O.moduli_chain(10, 3)
+    p = [int(v) for v in O.moduli_chain(10, 5)[0][3:5]]
+    pre = O.base_conv_precompute(q, p)
+    args = (ctx, 10, q, p, [int(v) for v in pre["qhinv"]], [int(v) for v in pre["qhmodp"]])
+    with pytest.raises(H.MathError):
+        H.BaseConverter(*args, kernel=3)
+    H.BaseConverter(*args, kernel=H.BCONV_KERNEL_WIDE).close()
+    qs, rs = O.moduli_chain(12, 6)
+    for opt in (H.KsOptions(H.PlanOptions(H.SPLIT_8_8, 0), 0, 0, 0, 0),  # a 2^16-only split at 2^12
+                H.KsOptions(H.PlanOptions(0, 0), 2, 0, 0, 0), H.KsOptions(H.PlanOptions(0, 0), 0, 3, 0, 0),
+                H.KsOptions(H.PlanOptions(0, 0), 0, 0, 0, 7)):
+        with pytest.raises(H.MathError):
+            H.KeySwitch(ctx, 12, qs[:4], rs[:4], qs[4:], rs[4:], 2, opt)
 
 
 def _generic_moduli(O, log_n, towers, bits=58):
