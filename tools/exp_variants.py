@@ -59,6 +59,7 @@ s = torch.cuda.current_stream()
 sp = vp(s.cuda_stream)
 times = {nm: {0: [], 1: [], 2: [], "all": [], "fwd": [], "inv": []} for nm, _, _ in libs}
 ref = None
+ref_t = {}
 for rnd in range(int(os.environ.get("EXP_ROUNDS", "6"))):
     # alternate the order every round (the first engine of a round has an edge)
     for nm, L, plan in (libs if rnd % 2 == 0 else libs[::-1]):
@@ -91,6 +92,10 @@ for rnd in range(int(os.environ.get("EXP_ROUNDS", "6"))):
             e1.synchronize()
             if rnd > 0:
                 times[nm][st].append(e0.elapsed_time(e1))
+            if st not in ref_t:
+                ref_t[st] = x
+            elif not torch.equal(ref_t[st], x):
+                print("MISMATCH", nm, st, flush=True)
         if ref is None:
             ref = c.clone()
         elif not torch.equal(ref, c):
