@@ -118,9 +118,10 @@ def parse_args(argv=None):
     ap.add_argument("--no-check", action="store_true")
     ap.add_argument("--no-extras", action="store_true",
                     help="headline only: skip configs[3]/[4]/[0], PCIe and CPU legs (profiling passes)")
-    ap.add_argument("--workload", default="pipeline", choices=["pipeline", "keyswitch"],
+    ap.add_argument("--workload", default="pipeline", choices=["pipeline", "keyswitch", "rescale", "bv_keyswitch"],
                     help="pipeline = the headline metric (configs[2]); keyswitch = configs[4] HYBRID "
-                         "key switching as the main line")
+                         "key switching as the main line; rescale / bv_keyswitch = callers outside SURVEY.md "
+                         "§8's rows (CKKS rescaling, BV key switching), measured only on request")
     ap.add_argument("--shard", default="batch", choices=["batch", "towers"],
                     help="batch = every rank runs its own batch of --batch (weak scaling, the default line); "
                          "towers = configs[3] as the main line: --towers split across ranks (strong scaling)")
@@ -164,13 +165,23 @@ def launch_ranks(n: int) -> int:
 def capi_status(records, world):
     """Top-level summary of how the evaluation keys travelled: capi is True only
     when every broadcast of the run used ofhe_hip_bcast_evalkey (None at N = 1:
-    nothing is broadcast); reasons name each fallback."""
+    nothing is broadcast); reasons name each fallback, then every rank whose
+    own C-ABI communicator failed (the records' "ranks", shard.key_broadcaster
+    .per_rank); per_rank lists, per broadcast, the ranks whose communicator
+    came up and those that did not."""
     recs = {k: v for k, v in records.items() if v}
     if world <= 1 or not recs:
-        return {"capi": None, "reasons": [], "broadcasts": sorted(recs)}
+        return {"capi": None, "reasons": [], "broadcasts": sorted(recs), "per_rank": {}}
     bad = {k: v.get("backend") for k, v in recs.items() if not v.get("capi")}
-    return {"capi": not bad, "reasons": [f"{k}: {why}" for k, why in sorted(bad.items())],
-            "broadcasts": sorted(recs)}
+    reasons = [f"{k}: {why}" for k, why in sorted(bad.items())]
+    per_rank = {}
+    for k, v in sorted(recs.items()):
+        ranks = v.get("ranks") or []
+        per_rank[k] = {"comm_up": sorted(r["rank"] for r in ranks if r.get("comm")),
+                       "comm_failed": sorted(r["rank"] for r in ranks if not r.get("comm"))}
+        reasons += [f"{k}: rank {r['rank']}: {r.get('error')}" for r in sorted(ranks, key=lambda r: r["rank"])
+                    if not r.get("comm")]
+    return {"capi": not bad, "reasons": reasons, "broadcasts": sorted(recs), "per_rank": per_rank}
 
 
 def capi_exit_code(status, require: bool) -> int:
@@ -194,7 +205,8 @@ def launch_check(args):
     bfn, backend, comm = shard.key_broadcaster(None, rank, world)
     key = torch.arange(64, dtype=torch.int64) if rank == 0 else torch.zeros(64, dtype=torch.int64)
     bfn(key, 0)
-    rec = {"backend": backend, "capi": comm is not None, "verified": shard.same_on_all_ranks(key)}
+    rec = {"backend": backend, "capi": comm is not None, "verified": shard.same_on_all_ranks(key),
+           "ranks": bfn.per_rank}
     status = capi_status({"launch_check": rec}, world)
     if rank == 0:
         print(json.dumps({"launch_check": True, "n_gpus": world, "ranks": [i["rank"] for i in info],
@@ -222,6 +234,8 @@ def main():
         sys.exit(launch_check(args))
     if args.workload == "keyswitch":
         sys.exit(bench_keyswitch_main(args))
+    if args.workload in ("rescale", "bv_keyswitch"):
+        sys.exit(bench_extra_main(args))
     sys.exit(bench_pipeline(args))
 
 
@@ -298,6 +312,22 @@ def load_pmc(log_n, towers, batch):
     return pm, None
 
 
+def headline_config(shard_mode, world, log_n, T_total, B):
+    """The line's config block.  batch: configs[2], every rank its own batch
+    of B; towers: configs[3], T_total towers split in contiguous ranges over
+    the ranks (rank 0's share is towers_rank0), the same B on every rank."""
+    import shard
+
+    if shard_mode == "batch":
+        return {"workload": f"configs[2]: N=2^{log_n}, towers={T_total}, batch={B} per GPU, c = INTT(NTT(a) (.) b)",
+                "log_n": log_n, "towers": T_total, "batch_per_gpu": B, "global_batch": B * world,
+                "parallelism": f"batch-sharded x{world} (no data-path collective)"}
+    return {"workload": f"configs[3]: N=2^{log_n}, towers={T_total} split over {world} GPUs, "
+                        f"batch={B}, c = INTT(NTT(a) (.) b)",
+            "log_n": log_n, "towers": T_total, "towers_rank0": shard.shard_towers(T_total, 0, world)[1],
+            "global_batch": B, "parallelism": f"tower-sharded x{world} (no data-path collective)"}
+
+
 def bench_pipeline(args):
     import torch
     import torch.distributed as dist
@@ -348,7 +378,7 @@ def bench_pipeline(args):
         bfn(key, 0)
         torch.cuda.synchronize()
         bcast = {"bytes": key.numel() * 8, "ms": (time.perf_counter() - t0) * 1e3, "backend": backend,
-                 "capi": comm is not None, "verified": shard.same_on_all_ranks(key)}
+                 "capi": comm is not None, "verified": shard.same_on_all_ranks(key), "ranks": bfn.per_rank}
         del key
 
     def step():
@@ -376,7 +406,7 @@ def bench_pipeline(args):
         ev1.synchronize()
         kernels_ms[STAGE_NAMES[st]] = ev0.elapsed_time(ev1) / reps
 
-    roofline = make_roofline(pipe_ms, kernels_ms, coeffs_rank, log_n, T, B)
+    roofline = make_roofline(pipe_ms, kernels_ms, coeffs_rank, log_n, T, B, ms_per_step=ms_per_step)
     power = power_sample(step, pipe_ms, local) if (rank == 0 and not args.no_extras) else None
 
     # spot parity check against the oracle (two (batch, tower) rows)
@@ -407,9 +437,8 @@ def bench_pipeline(args):
     extras = {}
     if not args.no_extras:
         extras["configs3"] = bench_configs3(args, ctx, world, rank, dev)
-        extras["keyswitch"] = bench_keyswitch(args, ctx, world, rank, dev, steps=args.ks_steps, warmup=2)
-        extras["rescale"] = bench_rescale(args, ctx, world, rank, dev, steps=args.ks_steps, warmup=2)
-        extras["bv_keyswitch"] = bench_bv(args, ctx, world, rank, dev, steps=5, warmup=1)
+        extras["keyswitch"] = bench_keyswitch(args, ctx, world, rank, dev, steps=args.ks_steps, warmup=2,
+                                              with_stages=True)
         if rank == 0 and world == 1:
             extras["pcie_inclusive"] = (pcie_inclusive(plan, args.pcie_batch, args.pcie_chunks, dev)
                                         if args.pcie_chunks > 0 else None)
@@ -433,15 +462,7 @@ def bench_pipeline(args):
             "dtype": "u64",
             "data": "synthetic: splitmix64 residues mod q_t, seed 0x5EED^(b<<20)^(t<<8)^operand "
                     "(SURVEY.md §8(d)), generated on the device; a coefficient form, b evaluation form",
-            "config": ({"workload": f"configs[2]: N=2^{log_n}, towers={T}, batch={B} per GPU, "
-                                    "c = INTT(NTT(a) (.) b)",
-                        "log_n": log_n, "towers": T, "batch_per_gpu": B, "global_batch": B * world,
-                        "parallelism": f"batch-sharded x{world} (no data-path collective)"}
-                       if args.shard == "batch" else
-                       {"workload": f"configs[3]: N=2^{log_n}, towers={T_total} split over {world} GPUs, "
-                                    f"batch={B}, c = INTT(NTT(a) (.) b)",
-                        "log_n": log_n, "towers": T_total, "towers_rank0": T, "global_batch": B,
-                        "parallelism": f"tower-sharded x{world} (no data-path collective)"}),
+            "config": headline_config(args.shard, world, log_n, T_total, B),
             "roofline": roofline,
             "kernels_ms": kernels_ms,
             "cpu_baseline": extras.get("cpu_baseline"),
@@ -452,8 +473,6 @@ def bench_pipeline(args):
             "secondary_ops": secondary,
             "configs3": extras.get("configs3"),
             "keyswitch": extras.get("keyswitch"),
-            "rescale": extras.get("rescale"),
-            "bv_keyswitch": extras.get("bv_keyswitch"),
             "configs0": extras.get("configs0"),
             "pcie_inclusive": extras.get("pcie_inclusive"),
             "build_id": build_id(),
@@ -537,21 +556,24 @@ def secondary_ops(plan, a, b, c, B, T, n, stream, reps=3):
     return out
 
 
-def make_roofline(pipe_ms, kernels_ms, coeffs_rank, log_n, T, B):
-    """Roofline of the dominant kernel (the task's contract: ALGORITHMIC bytes
-    per launch over that kernel's average launch duration, HIP events on the
-    launch stream) at the top level, with the metric op as a whole (NTT +
-    Hadamard + INTT, three launches; the north star's 40 % target is stated on
-    it) under "pipeline" and every launch under "kernels".  HBM: algorithmic
-    bytes (16 / 24 / 16 B per coefficient for the three launches, 24 for the
-    pipeline).  VALU: the measured VALU instructions per
-    coefficient (SQ_INSTS_VALU, profiles/pmc_current.json, same build and
-    configuration) at the measured clock and the 0.25 wave64 instructions per
-    SIMD per cycle issue ceiling give the VALU-bound time; its ratio to the
-    measured time is the VALU fraction.  `bound` is the roof the counters put
-    closer (the larger fraction): "valu" for these kernels, which the task's
-    "hbm" | "mfma" does not name (gfx950 has no 64-bit integer multiplier and
-    the path runs no matrix instructions)."""
+def make_roofline(pipe_ms, kernels_ms, coeffs_rank, log_n, T, B, ms_per_step=None):
+    """Roofline of the metric op, the unit the north star's >= 0.40 target is
+    stated on (schema 3, round 6): 24 algorithmic B per coefficient (read a,
+    read b, write c) x the coefficients one GPU processes per
+    step / ms_per_step (the timed region; HIP-event time of the same three
+    launches when ms_per_step is not given).  The op is three launches back to
+    back, so `traffic` is the three launches' PMC HBM bytes per step.  Beside
+    it: the dominant kernel (its own algorithmic bytes per launch over its
+    average launch duration, HIP events on the launch stream; schema 2's
+    top-level figure, now `dominant_kernel_frac`), and every launch under
+    "kernels".  VALU: the measured VALU instructions per coefficient
+    (SQ_INSTS_VALU, profiles/pmc_current.json, same build and configuration)
+    at the measured clock and the 0.25 wave64 instructions per SIMD per cycle
+    issue ceiling give the VALU-bound time; its ratio to the measured time is
+    the VALU fraction.  `bound` is the roof the counters put closer: "valu"
+    for these kernels, which the task's "hbm" | "mfma" does not name (gfx950
+    has no 64-bit integer multiplier and the path runs no matrix
+    instructions, DESIGN.md (d))."""
     pm, why = load_pmc(log_n, T, B)
     pk = (pm or {}).get("kernels", {})
     kernels = {}
@@ -579,33 +601,35 @@ def make_roofline(pipe_ms, kernels_ms, coeffs_rank, log_n, T, B):
         ent["bound"] = (("valu" if ent["valu"]["valu_frac"] > ent["hbm_frac"] else "hbm")
                         if ent["valu"] else None)
         kernels[name] = ent
+    step_ms = ms_per_step if ms_per_step else pipe_ms
     alg = ALG_BYTES_PER_COEFF * coeffs_rank
-    achieved = alg / (pipe_ms * 1e-3) / 1e9
+    achieved = alg / (step_ms * 1e-3) / 1e9
     hbm_frac = achieved / HBM_PEAK_GBS
     valu = None
     if valu_ok and valu_ms_total > 0:
-        valu = {"valu_bound_ms": valu_ms_total, "frac": valu_ms_total / pipe_ms,
+        valu = {"valu_bound_ms": valu_ms_total, "frac": valu_ms_total / step_ms,
                 "lane_insts_per_coeff": sum(kernels[k]["valu"]["lane_insts_per_coeff"] for k in kernels),
                 "issue_ceiling": VALU_ISSUE_CEILING, "simds": SIMDS,
                 "source": "profiles/pmc_current.json (tools/pmc_round.sh, SQ_INSTS_VALU + GRBM_GUI_ACTIVE)"}
-    pipeline = {"bound": ("valu" if valu["frac"] > hbm_frac else "hbm") if valu else None,
-                "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": hbm_frac,
-                "traffic": traffic_total if (pk and all(kernels[k]["traffic"] for k in kernels)) else None,
-                "scope": "c = INTT(NTT(a) (.) b), 3 launches (forward column pass, fused block pass, "
-                         "inverse column pass); the north star's >= 0.40 target is stated on this",
-                "alg_bytes_per_step": alg, "ms_per_step_events": pipe_ms, "valu": valu}
+    traffic = traffic_total if (pk and all(kernels[k]["traffic"] for k in kernels)) else None
+    bound = ("valu" if valu["frac"] > hbm_frac else "hbm") if valu else None
     dominant = max(kernels_ms, key=kernels_ms.get)
     d = kernels[dominant]
-    # schema 2 (round 3 on): the top-level figures are the dominant kernel's;
-    # round 2's top-level (whole three-launch pipeline) is "pipeline_frac" /
-    # "pipeline", so records stay comparable across rounds
-    return {"schema": 2, "bound": d["bound"], "achieved": d["achieved_gbs"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": d["hbm_frac"], "traffic": d["traffic"], "dominant_kernel": dominant,
-            "pipeline_frac": hbm_frac,
-            "scope": f"dominant kernel {dominant}: {KERNEL_BYTES[dominant]} algorithmic B per coefficient x "
-                     f"{coeffs_rank} coefficients per launch / its average launch duration (HIP events)",
-            "valu": d["valu"], "pipeline": pipeline, "kernels": kernels,
-            "counters": "matched" if pm else why}
+    return {"schema": 3, "bound": bound, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": hbm_frac, "traffic": traffic,
+            "scope": f"the metric op c = INTT(NTT(a) (.) b) on one GPU: {ALG_BYTES_PER_COEFF} algorithmic B per "
+                     f"coefficient x {coeffs_rank} coefficients per step / ms per step (three launches: forward "
+                     "column pass, fused block pass, inverse column pass; traffic = their PMC HBM bytes per step); "
+                     "the north star's >= 0.40 target is stated on this",
+            "alg_bytes_per_step": alg, "ms_per_step": step_ms, "ms_per_step_events": pipe_ms,
+            "pipeline_frac": hbm_frac, "valu": valu,
+            "dominant_kernel": dominant, "dominant_kernel_frac": d["hbm_frac"],
+            "dominant_kernel_achieved": d["achieved_gbs"], "dominant_kernel_ms": d["ms"],
+            "dominant_kernel_traffic": d["traffic"],
+            "dominant_kernel_scope": f"{dominant}: {KERNEL_BYTES[dominant]} algorithmic B per coefficient x "
+                                     f"{coeffs_rank} coefficients per launch / its average launch duration "
+                                     "(HIP events on the launch stream)",
+            "kernels": kernels, "counters": "matched" if pm else why}
 
 
 # ---------------------------------------------------------------------------
@@ -777,7 +801,7 @@ def bench_keyswitch(args, ctx, world, rank, dev, steps, warmup, with_stages=Fals
         bfn(kb, 0)
         bfn(ka, 0)
         key_bcast = {"backend": backend, "capi": comm is not None,
-                     "verified": shard.same_on_all_ranks(kb) and shard.same_on_all_ranks(ka)}
+                     "verified": shard.same_on_all_ranks(kb) and shard.same_on_all_ranks(ka), "ranks": bfn.per_rank}
     o0 = torch.empty((B, sq, n), dtype=torch.int64, device=dev)
     o1 = torch.empty_like(o0)
 
@@ -785,12 +809,23 @@ def bench_keyswitch(args, ctx, world, rank, dev, steps, warmup, with_stages=Fals
         ks.core(sq, c.data_ptr(), kb.data_ptr(), ka.data_ptr(), o0.data_ptr(), o1.data_ptr(), 0, B, sptr)
 
     elapsed, ev_ms = _timed(step, steps, warmup, stream, world, dev)
-    stages = None
+    stages, roof = None, None
     if with_stages:
         digits = torch.empty((B, beta, sq + sp_, n), dtype=torch.int64, device=dev)
         ct = torch.empty((2, B, sq + sp_, n), dtype=torch.int64, device=dev)
         stages = {}
         reps = max(2, min(steps, 5))
+
+        def ev_time(fn):
+            fn()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            for _ in range(reps):
+                fn()
+            e1.record(stream)
+            e1.synchronize()
+            return e0.elapsed_time(e1) / reps
+
         calls = {
             "mod_up(precompute)": lambda: ks.precompute(sq, c.data_ptr(), digits.data_ptr(), B, sptr),
             "inner_product": lambda: ks.fast_core_ext(sq, digits.data_ptr(), kb.data_ptr(), ka.data_ptr(),
@@ -799,14 +834,14 @@ def bench_keyswitch(args, ctx, world, rank, dev, steps, warmup, with_stages=Fals
                                      ks.mod_down(sq, ct[1].data_ptr(), o1.data_ptr(), 0, B, sptr)),
         }
         for name, fn in calls.items():
-            fn()
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record(stream)
-            for _ in range(reps):
-                fn()
-            e1.record(stream)
-            e1.synchronize()
-            stages[name] = e0.elapsed_time(e1) / reps
+            stages[name] = ev_time(fn)
+        # the standalone transform rate at this ring (the Q|P plan over the
+        # digits buffer: B * beta polynomials of Q + P towers), forward and inverse
+        tw = B * beta * (sq + sp_) * n
+        ntt_fwd_ms = ev_time(lambda: pqp.forward(digits.data_ptr(), B * beta, sptr))
+        ntt_inv_ms = ev_time(lambda: pqp.inverse(digits.data_ptr(), B * beta, sptr))
+        roof = keyswitch_roofline(sq, sp_, dnum, n, B, ev_ms, stages, tw / (ntt_fwd_ms * 1e-3),
+                                  tw / (ntt_inv_ms * 1e-3))
         del digits, ct
     # minimum HBM words per ciphertext polynomial and tower-coefficient: read c
     # (Q), write + read the digits (2 beta (Q+P)), write ct0/ct1 (2 (Q+P)),
@@ -831,7 +866,41 @@ def bench_keyswitch(args, ctx, world, rank, dev, steps, warmup, with_stages=Fals
                        "batch_per_gpu": B, "global_batch": B * world,
                        "parallelism": f"ciphertext-batch-sharded x{world}, key broadcast over RCCL"},
             "alg_hbm_gbs": alg_words * 8 * n * B / (elapsed / steps) / 1e9, "stages_ms": stages,
-            "evalkey_broadcast": key_bcast}
+            "roofline": roof, "evalkey_broadcast": key_bcast}
+
+
+def keyswitch_roofline(sq, sp, dnum, n, B, step_ms, stages, fwd_rate, inv_rate):
+    """configs[4]'s key switch against its own bound (round 6): the NTTs it
+    must run, at the standalone transform rate measured at this ring on this
+    GPU (the path is bound by integer VALU issue), plus the key
+    inner product's words at the 8 TB/s HBM peak.  Per ciphertext polynomial
+    at level l = sq (keyswitch-hybrid.cpp:330-482): digit j (cnt_j of alpha
+    towers) -> INTT of its cnt_j towers, NTT of the l - cnt_j + P complement
+    towers; each of the two ApproxModDowns -> INTT of P towers, NTT of l
+    towers.  Inner product HBM bytes per step: the digits B*beta*(l+P) towers
+    read, the keys 2*beta*(l+P) (shared by the batch) read, ct0/ct1 2*B*(l+P)
+    written, N words of 8 B each."""
+    alpha = -(-sq // dnum)
+    beta = min(-(-sq // alpha), dnum)
+    cnts = [min(alpha, sq - alpha * j) for j in range(beta)]
+    n_inv = sum(cnts) + 2 * sp
+    n_fwd = sum(sq - c + sp for c in cnts) + 2 * sq
+    transforms_ms = B * n * (n_fwd / fwd_rate + n_inv / inv_rate) * 1e3
+    ip_bytes = 8 * n * (sq + sp) * (B * beta + 2 * beta + 2 * B)
+    ip_bound_ms = ip_bytes / (HBM_PEAK_GBS * 1e9) * 1e3
+    bound_ms = transforms_ms + ip_bound_ms
+    ip = stages.get("inner_product")
+    return {"bound": "valu (transforms) + hbm (inner product)", "bound_ms": bound_ms, "ms_per_step": step_ms,
+            "frac": bound_ms / step_ms,
+            "transforms_per_keyswitch": {"ntt": n_fwd, "intt": n_inv, "total": n_fwd + n_inv},
+            "ntt_rate_coeffs_per_s": {"fwd": fwd_rate, "inv": inv_rate},
+            "transforms_ms": transforms_ms,
+            "inner_product": {"alg_bytes": ip_bytes, "bound_ms": ip_bound_ms, "ms": ip,
+                              "achieved_gbs": ip_bytes / (ip * 1e-3) / 1e9 if ip else None,
+                              "hbm_frac": ip_bytes / (ip * 1e-3) / 1e9 / HBM_PEAK_GBS if ip else None},
+            "scope": f"batch {B} ciphertext polynomials, N=2^{n.bit_length() - 1}, Q={sq}, P={sp}, dnum={dnum}: "
+                     "the transforms at the standalone NTT rate measured here plus the inner product at 8 TB/s, "
+                     "over the measured time per step (base conversion and element passes not in the bound)"}
 
 
 def bench_keyswitch_main(args):
@@ -854,6 +923,29 @@ def bench_keyswitch_main(args):
         dist.barrier()
         dist.destroy_process_group()
     return capi_exit_code(status, args.require_capi_comm)
+
+
+def bench_extra_main(args):
+    """--workload rescale | bv_keyswitch: one of the round-2 callers outside
+    SURVEY.md §8's rows as its own JSON line (not part of the default run)."""
+    import torch.distributed as dist
+
+    world, rank, local, dev = _dist_setup(args.dist_backend)
+    import ofhe_hip as H
+
+    ctx = H.Context(local)
+    if args.workload == "rescale":
+        out = bench_rescale(args, ctx, world, rank, dev, steps=args.steps, warmup=args.warmup)
+    else:
+        out = bench_bv(args, ctx, world, rank, dev, steps=args.steps, warmup=args.warmup)
+    if rank == 0:
+        out.update({"metric": out["workload"], "n_gpus": world, "higher_is_better": True, "vs_baseline": None,
+                    "dtype": "u64", "data": "synthetic: splitmix64 residues (SURVEY.md §8(d) seeds)"})
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    return 0
 
 
 # ---------------------------------------------------------------------------

@@ -92,6 +92,15 @@ int ofhe_hip_copy_to_host(ofhe_ctx_t ctx, void* dst, const void* src, size_t byt
 int ofhe_hip_copy_device(ofhe_ctx_t ctx, void* dst, const void* src, size_t bytes, void* stream);
 /* PimManager::start_kernel is synchronous (PimManager.h:68); here explicit. */
 int ofhe_hip_sync(ofhe_ctx_t ctx, void* stream);
+/* A completion marker on one stream.  The reference's copies block until the
+ * transfer is done (PimManager::copy_to_pim / copy_from_pim, PimManager.cpp:5-54);
+ * with an event the host waits for one staged DMA only, not for every launch
+ * queued on the stream (the C++ adapter's pinned staging, ofhe_dcrt.hpp). */
+typedef struct ofhe_event_s* ofhe_event_t;
+int ofhe_hip_event_create(ofhe_ctx_t ctx, ofhe_event_t* event);
+int ofhe_hip_event_record(ofhe_event_t event, void* stream); /* marks the stream's work so far */
+int ofhe_hip_event_sync(ofhe_event_t event);                 /* waits for the marked work     */
+int ofhe_hip_event_destroy(ofhe_event_t event);
 /* Return all but keep_bytes of the context's stream-ordered pool (scratch and
  * ofhe_hip_alloc_async blocks kept across synchronisations) to the device; the
  * reference frees DPU memory per call (PimManager::deallocate, PimManager.h:83-85). */
@@ -244,7 +253,9 @@ enum {
     OFHE_BCONV_KERNEL_WIDE = 2  /* 128-bit sums on the VALU, any number of sources         */
 };
 typedef struct ofhe_bconv_options {
-    uint32_t kernel;        /* OFHE_BCONV_KERNEL_*                                          */
+    uint32_t kernel;        /* OFHE_BCONV_KERNEL_*; LIMB / WIDE hold on every path that
+                               uses the converter (ApproxModUp / ApproxModDown at 2^17
+                               then run conversion and column pass as two kernels)     */
     uint32_t separate_cols; /* 1: in ofhe_hip_approx_mod_up / _down at N = 2^17, the
                                conversion and the targets' forward column pass as two
                                kernels instead of the fused k_bconv_cols                  */

@@ -777,13 +777,30 @@ static void register_tests() {
             EXPECT_EQ(Y.GetParams()->Moduli(), q, "moduli restored");
             EXPECT_EQ(Y.GetParams()->Roots(), P->Roots(), "roots restored");
             EXPECT_EQ(Y, X, "values restored");
-            // corrupt: a value >= q, a truncated stream
+            // corrupt: a value > q, a truncated stream
             std::string bad = bytes;
-            const uint64_t big = q[0];
+            const uint64_t big = q[0] + 1;
             std::memcpy(&bad[16], &big, 8);
             std::stringstream sb(bad), st(bytes.substr(0, bytes.size() - 5));
-            EXPECT_THROW(DCRTPolyHip::Load(sb, batch), deserialize_error, "non-canonical value");
+            EXPECT_THROW(DCRTPolyHip::Load(sb, batch), deserialize_error, "value above the modulus");
             EXPECT_THROW(DCRTPolyHip::Load(st, batch), deserialize_error, "truncated stream");
+        }
+        // a coefficient-form AutomorphismTransform keeps a negated zero as q
+        // (ofhe_hip.h): such an output saves and loads back word for word
+        {
+            std::vector<uint64_t> z((size_t)T * n, 0);
+            for (size_t i = 0; i < z.size(); i += 3) z[i] = 1 + rng() % (q[(i / n) % T] - 1);
+            DCRTPolyHip X(P, Format::COEFFICIENT);
+            X.SetValues(z, Format::COEFFICIENT);
+            DCRTPolyHip R = X.AutomorphismTransform(2 * n - 1);
+            const auto rv = R.GetValues();
+            size_t at_q = 0;
+            for (size_t i = 0; i < rv.size(); i++) at_q += rv[i] == q[(i / n) % T];
+            EXPECT_EQ(at_q > 0, true, "the automorphism output holds the representative q");
+            std::stringstream ss;
+            R.Save(ss);
+            DCRTPolyHip Y = DCRTPolyHip::Load(ss);
+            EXPECT_EQ(Y.GetValues(), rv, "q representatives survive Save -> Load");
         }
         // two records over different bases cannot form one batch
         std::stringstream mix;

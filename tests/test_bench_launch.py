@@ -43,29 +43,36 @@ def test_roofline_uses_only_matching_counters(tmp_path, monkeypatch):
     kms = {"colpass<fwd>": 3.2, "k_block<fused>": 6.8, "colpass<inv>": 3.4}
     coeffs = 1024 * 16 * 65536
     monkeypatch.setattr(bench, "PMC_FILE", str(tmp_path / "none.json"))
-    r = bench.make_roofline(13.5, kms, coeffs, 16, 16, 1024)
+    r = bench.make_roofline(13.5, kms, coeffs, 16, 16, 1024, ms_per_step=13.6)
     assert r["bound"] is None and r["valu"] is None and r["traffic"] is None
-    # top level: the dominant kernel's algorithmic bytes over its launch time
+    # top level (schema 3): the metric op, 24 algorithmic B per coefficient over
+    # the timed region's ms per step -- the figure the north star's 0.40 is on
+    assert r["schema"] == 3
+    assert abs(r["frac"] - 24 * coeffs / 13.6e-3 / 8e12) < 1e-12
+    assert r["pipeline_frac"] == r["frac"] and abs(r["achieved"] / 8000 - r["frac"]) < 1e-12
+    # the dominant kernel beside it: its algorithmic bytes over its launch time
     assert r["dominant_kernel"] == "k_block<fused>"
-    assert abs(r["frac"] - 24 * coeffs / 6.8e-3 / 8e12) < 1e-9
-    assert abs(r["pipeline"]["frac"] - 24 * coeffs / 13.5e-3 / 8e12) < 1e-9
+    assert abs(r["dominant_kernel_frac"] - 24 * coeffs / 6.8e-3 / 8e12) < 1e-12
+    # without ms_per_step the op's event time stands in
+    assert abs(bench.make_roofline(13.5, kms, coeffs, 16, 16, 1024)["frac"] - 24 * coeffs / 13.5e-3 / 8e12) < 1e-12
     pm = {"build_id": bench.build_id(), "config": {"log_n": 16, "towers": 16, "batch": 1024},
           "kernels": {k: {"hbm_bytes_per_launch": bench.KERNEL_BYTES[k] * coeffs, "valu_insts_per_coeff": ipc,
                           "clock_ghz": 1.6} for k, ipc in zip(kms, (86, 181, 98))}}
     f = tmp_path / "pmc.json"
     f.write_text(json.dumps(pm))
     monkeypatch.setattr(bench, "PMC_FILE", str(f))
-    r = bench.make_roofline(13.5, kms, coeffs, 16, 16, 1024)
-    assert r["counters"] == "matched" and r["bound"] == "valu" and r["pipeline"]["bound"] == "valu"
-    assert r["traffic"] == 24 * coeffs
-    assert r["pipeline"]["traffic"] == sum(bench.KERNEL_BYTES[k] * coeffs for k in kms)
+    r = bench.make_roofline(13.5, kms, coeffs, 16, 16, 1024, ms_per_step=13.5)
+    assert r["counters"] == "matched" and r["bound"] == "valu"
+    assert r["dominant_kernel_traffic"] == 24 * coeffs
+    assert r["traffic"] == sum(bench.KERNEL_BYTES[k] * coeffs for k in kms)
     want = (86 + 181 + 98) * coeffs / 64 / (1024 * 1.6e9 * 0.25) * 1e3
-    assert abs(r["pipeline"]["valu"]["valu_bound_ms"] - want) < 1e-9
-    assert abs(r["valu"]["valu_bound_ms"] - 181 * coeffs / 64 / (1024 * 1.6e9 * 0.25) * 1e3) < 1e-9
+    assert abs(r["valu"]["valu_bound_ms"] - want) < 1e-9 and abs(r["valu"]["frac"] - want / 13.5) < 1e-12
+    assert abs(r["kernels"]["k_block<fused>"]["valu"]["valu_bound_ms"] -
+               181 * coeffs / 64 / (1024 * 1.6e9 * 0.25) * 1e3) < 1e-9
     pm["build_id"] = "stale"
     f.write_text(json.dumps(pm))
     r = bench.make_roofline(13.5, kms, coeffs, 16, 16, 1024)
-    assert r["valu"] is None and r["pipeline"]["valu"] is None and "stale" in r["counters"]
+    assert r["valu"] is None and "stale" in r["counters"]
     pm["build_id"] = bench.build_id()
     pm["config"]["batch"] = 256
     f.write_text(json.dumps(pm))
@@ -89,8 +96,35 @@ def test_require_capi_comm_fires_on_fallback():
         assert (r.returncode == 0) == ok, (flag, r.returncode, r.stderr[-2000:])
 
 
+def test_launch_check_reports_every_rank():
+    """Each rank's own communicator outcome reaches the line: on a CPU box no
+    rank has a device context, so both appear under comm_failed with the
+    error each one raised."""
+    r = subprocess.run([sys.executable, BENCH, "--gpus", "2", "--launch-check"], capture_output=True, text=True,
+                       timeout=240, env=_env())
+    assert r.returncode == 0, r.stderr[-2000:]
+    out = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
+    ranks = out["evalkey_broadcast"]["ranks"]
+    assert sorted(x["rank"] for x in ranks) == [0, 1]
+    assert all(not x["comm"] and "no device context" in x["error"] for x in ranks)
+    st = out["evalkey_broadcast_capi"]
+    assert st["per_rank"]["launch_check"] == {"comm_up": [], "comm_failed": [0, 1]}
+    assert any("rank 1: no device context" in why for why in st["reasons"])
+
+
 def test_capi_status_bookkeeping():
     import bench
+
+    # per-rank outcomes: rank 3 alone failed -> capi False, rank 3 named
+    ranks = [{"rank": i, "comm": i != 3, "error": None if i != 3 else "ncclCommInitRank: unhandled"} for i in range(8)]
+    st = bench.capi_status({"headline": {"backend": "torch.distributed nccl (C-ABI comm: peer)", "capi": False,
+                                         "ranks": ranks}}, 8)
+    assert st["capi"] is False
+    assert st["per_rank"]["headline"] == {"comm_up": [0, 1, 2, 4, 5, 6, 7], "comm_failed": [3]}
+    assert st["reasons"][-1] == "headline: rank 3: ncclCommInitRank: unhandled"
+    up = [{"rank": i, "comm": True, "error": None} for i in range(8)]
+    st = bench.capi_status({"headline": {"backend": "ofhe_hip_bcast_evalkey (RCCL)", "capi": True, "ranks": up}}, 8)
+    assert st["capi"] is True and st["reasons"] == [] and st["per_rank"]["headline"]["comm_up"] == list(range(8))
 
     assert bench.capi_status({"headline": None}, 1)["capi"] is None
     good = {"backend": "ofhe_hip_bcast_evalkey (RCCL)", "capi": True}
@@ -124,3 +158,18 @@ def test_power_sample_parses_rocm_smi(monkeypatch):
     r = bench.power_sample(lambda: calls.append(1), 10.0, 0, seconds=0.5)
     assert r["package_w"] == 1391.0 and r["cap_w"] == 1400.0 and r["sclk_mhz"] == 1946.0 and r["under_load"]
     assert len(calls) == r["steps_queued"] == 50
+
+
+def test_configs3_line_at_eight_ranks():
+    """bench.py --gpus 8 --shard towers --towers 32 --batch 512 (configs[3]):
+    rank 0 owns 4 towers, the block names them, and the line's evaluation-key
+    broadcast record carries every rank's communicator outcome (the record
+    shape test_launch_check_reports_every_rank checks end to end)."""
+    import bench
+
+    args = bench.parse_args(["--gpus", "8", "--shard", "towers", "--towers", "32", "--batch", "512"])
+    c = bench.headline_config(args.shard, 8, args.log_n, args.towers, args.batch)
+    assert c["towers_rank0"] == 4 and c["towers"] == 32 and c["global_batch"] == 512
+    assert c["workload"].startswith("configs[3]") and "tower-sharded x8" in c["parallelism"]
+    c = bench.headline_config("batch", 8, 16, 16, 1024)
+    assert c["global_batch"] == 8 * 1024 and c["batch_per_gpu"] == 1024

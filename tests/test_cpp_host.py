@@ -97,13 +97,35 @@ def test_cpp_device_resident_chain(tmp_path):
 
 
 @gpu
-def test_cpp_openfhe_hooks():
-    """The RUN_ON_HIP hook bodies (host/ofhe_openfhe_hooks.hpp) instantiated on a
-    tower type with the reference's accessor names, checked against the oracle
-    (tests/cpp/test_hooks.cpp)."""
+def test_cpp_openfhe_hooks(tmp_path):
+    """The RUN_ON_HIP hook bodies (host/ofhe_openfhe_hooks.hpp) inside a test
+    double of DCRTPolyImpl / KeySwitchHYBRID with the reference's accessor
+    names (tests/cpp/mock_openfhe.hpp), with the gate forced to the device and
+    to the CPU loop, each checked against the oracle (tests/cpp/test_hooks.cpp).
+    The KeySwitchCore hook's device results (two levels, t = 0 and a BGV t)
+    are dumped and checked here against oracle/keyswitch.py."""
+    import numpy as np
+
+    import keyswitch as K
+
     d = os.path.join(ROOT, "tests", "cpp")
     subprocess.run(["make", "-s", "-C", d], check=True)
-    r = subprocess.run([os.path.join(d, "test_hooks_bin")], capture_output=True, text=True, timeout=300)
+    out = str(tmp_path / "ks.bin")
+    r = subprocess.run([os.path.join(d, "test_hooks_bin"), out], capture_output=True, text=True, timeout=300)
     print(r.stdout)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "hooks: 0 failures" in r.stdout
+    v = _read_chain(out)
+    log_n, sq, sp, dnum = (int(x) for x in v[0])
+    n = 1 << log_n
+    allq, allr = [int(x) for x in v[1]], [int(x) for x in v[2]]
+    kb, ka = v[3].reshape(dnum, sq + sp, n), v[4].reshape(dnum, sq + sp, n)
+    kp = K.KeySwitchParams(n, allq[:sq], allr[:sq], allq[sq:], allr[sq:], dnum)
+    cases = v[5:]
+    assert len(cases) == 4 * 4
+    for i in range(0, len(cases), 4):
+        l, t = (int(x) for x in cases[i])
+        c = cases[i + 1].reshape(1, l, n)
+        r0, r1 = K.ks_core(kp, c, kb, ka, t)
+        assert np.array_equal(cases[i + 2].reshape(1, l, n), r0), f"KeySwitchCore hook ct0, l={l} t={t}"
+        assert np.array_equal(cases[i + 3].reshape(1, l, n), r1), f"KeySwitchCore hook ct1, l={l} t={t}"

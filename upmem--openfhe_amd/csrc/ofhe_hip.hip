@@ -141,9 +141,13 @@ int ofhe_hip_free_async(ofhe_ctx_t ctx, void* dptr, void* stream) {
     if (!dptr) return OFHE_OK;
     HIPCHK(hipSetDevice(ctx->device));
     std::lock_guard<std::mutex> lk(ctx->blocks_mu);
-    if (!ctx->async_blocks.erase(dptr))
+    auto it = ctx->async_blocks.find(dptr);
+    if (it == ctx->async_blocks.end())
         return fail(OFHE_ERR_ARG, "ofhe_hip_free_async: not a live ofhe_hip_alloc_async block of this context");
+    // untracked only once the pool has it back: a failed free leaves the block
+    // live, so ofhe_hip_finalize still refuses to destroy the pool under it
     HIPCHK(hipFreeAsync(dptr, pick(stream)));
+    ctx->async_blocks.erase(it);
     return OFHE_OK;
 }
 
@@ -191,6 +195,43 @@ int ofhe_hip_copy_device(ofhe_ctx_t ctx, void* dst, const void* src, size_t byte
 int ofhe_hip_sync(ofhe_ctx_t ctx, void* stream) {
     if (!ctx) return fail(OFHE_ERR_ARG, "ctx is NULL");
     HIPCHK(hipStreamSynchronize(pick(stream)));
+    return OFHE_OK;
+}
+
+// A completion marker on one stream: waiting on it waits for that stream's
+// work up to the record, nothing queued after it (the adapter's staging
+// buffers are reused once their DMA has read them, ofhe_dcrt.hpp).
+struct ofhe_event_s {
+    ofhe_ctx_t ctx = nullptr;
+    hipEvent_t ev = nullptr;
+};
+
+int ofhe_hip_event_create(ofhe_ctx_t ctx, ofhe_event_t* out) {
+    if (!ctx || !out) return fail(OFHE_ERR_ARG, "NULL argument");
+    HIPCHK(hipSetDevice(ctx->device));
+    hipEvent_t e = nullptr;
+    HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    *out = new ofhe_event_s{ctx, e};
+    return OFHE_OK;
+}
+
+int ofhe_hip_event_record(ofhe_event_t ev, void* stream) {
+    if (!ev) return fail(OFHE_ERR_ARG, "event is NULL");
+    HIPCHK(hipEventRecord(ev->ev, pick(stream)));
+    return OFHE_OK;
+}
+
+int ofhe_hip_event_sync(ofhe_event_t ev) {
+    if (!ev) return fail(OFHE_ERR_ARG, "event is NULL");
+    HIPCHK(hipEventSynchronize(ev->ev));
+    return OFHE_OK;
+}
+
+int ofhe_hip_event_destroy(ofhe_event_t ev) {
+    if (!ev) return fail(OFHE_ERR_ARG, "event is NULL");
+    (void)hipSetDevice(ev->ctx->device);
+    (void)hipEventDestroy(ev->ev);
+    delete ev;
     return OFHE_OK;
 }
 
@@ -1155,8 +1196,11 @@ int ofhe_hip_bconv_destroy(ofhe_bconv_t b) {
 }
 
 namespace ofhe {
+// A converter created with an explicit kernel (ofhe_bconv_options.kernel LIMB /
+// WIDE) runs that kernel on every path, the fused ModUp / ModDown column
+// kernel included: only OFHE_BCONV_KERNEL_AUTO may take k_bconv_cols.
 bool bconv_cols_ok(ofhe_plan_t p, const BconvArgs& B) {
-    return OFHE_BCONV_MMA && p && p->log_n == 17 && B.log_n == 17 && p->split == SPLIT_COLS && B.mm_tab &&
+    return OFHE_BCONV_MMA && B.kernel == OFHE_BCONV_KERNEL_AUTO && p && p->log_n == 17 && B.log_n == 17 && p->split == SPLIT_COLS && B.mm_tab &&
            B.mm_ks >= 1 && B.mm_ks <= 4 && (B.mm_spq != 0) == p->spq;
 }
 

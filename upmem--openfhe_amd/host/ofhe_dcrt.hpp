@@ -88,35 +88,53 @@ public:
     void deallocate(void* p) { check(ofhe_hip_free_async(ctx_, p, nullptr), "HipManager::deallocate"); }
     void zero(void* dst, size_t bytes) { check(ofhe_hip_zero(ctx_, dst, bytes, nullptr), "HipManager::zero"); }
     // Host <-> device copies of the caller's (pageable) memory go through the
-    // manager's pinned staging buffer: one DMA from page-locked memory on the
-    // stream, in the stream's order, then a wait, so the caller's buffer and
-    // the staging buffer are free again when the call returns -- the
-    // synchronous copy_to_pim / copy_from_pim of PimManager.cpp:5-54.  No
-    // pageable hipMemcpyAsync: that path's staging and ordering are the HIP
-    // runtime's own (round 4's driver record read back stale words on it,
-    // DESIGN.md (c) "The round-4 adapter failure").
+    // manager's two pinned staging buffers: the caller's words are copied into
+    // one, a DMA from page-locked memory is queued on the stream (in the
+    // stream's order, after the launches that produce or read `dst`), and an
+    // event marks it.  A buffer is refilled only after the event of its last
+    // DMA -- a wait for that one transfer, not for every launch queued on the
+    // stream (round 5 drained the whole stream before and after each round).
+    // copy_to_device returns once the caller's buffer has been read (the
+    // copy_to_pim contract, PimManager.cpp:5-37), with the DMA possibly still
+    // in flight; copy_from_device returns with the words in `dst`
+    // (copy_from_pim, PimManager.cpp:39-54), overlapping each chunk's DMA
+    // with the previous chunk's host copy.  No pageable hipMemcpyAsync: that
+    // path's staging and ordering are the HIP runtime's own (round 4's driver
+    // record read back stale words on it, DESIGN.md (c) "The round-4 adapter
+    // failure").
     void copy_to_device(void* dst, const void* src, size_t bytes) {
         std::lock_guard<std::mutex> lk(stage_mu_);
-        sync();  // queued work that reads dst has finished
+        const size_t room = stage_room(bytes);
         for (size_t off = 0; off < bytes;) {
-            const size_t n = std::min(bytes - off, stage_room(bytes - off));
-            std::memcpy(stage_, static_cast<const char*>(src) + off, n);
-            check(ofhe_hip_copy_to_device(ctx_, static_cast<char*>(dst) + off, stage_, n, nullptr),
+            const size_t n = std::min(bytes - off, room);
+            const int k = next_;
+            next_ ^= 1;
+            stage_wait(k);  // the buffer's previous DMA has read it
+            std::memcpy(stage_[k], static_cast<const char*>(src) + off, n);
+            check(ofhe_hip_copy_to_device(ctx_, static_cast<char*>(dst) + off, stage_[k], n, nullptr),
                   "HipManager::copy_to_device");
-            sync();  // the DMA has read the staging buffer
+            stage_mark(k);
             off += n;
         }
     }
     void copy_from_device(void* dst, const void* src, size_t bytes) {
         std::lock_guard<std::mutex> lk(stage_mu_);
+        const size_t room = stage_room(bytes);
+        size_t prev_off = 0, prev_n = 0;
+        int prev = -1;
         for (size_t off = 0; off < bytes;) {
-            const size_t n = std::min(bytes - off, stage_room(bytes - off));
-            check(ofhe_hip_copy_to_host(ctx_, stage_, static_cast<const char*>(src) + off, n, nullptr),
+            const size_t n = std::min(bytes - off, room);
+            const int k = next_;
+            next_ ^= 1;
+            stage_wait(k);
+            check(ofhe_hip_copy_to_host(ctx_, stage_[k], static_cast<const char*>(src) + off, n, nullptr),
                   "HipManager::copy_from_device");
-            sync();  // queued producers, then the DMA, have finished
-            std::memcpy(static_cast<char*>(dst) + off, stage_, n);
+            stage_mark(k);
+            if (prev >= 0) drain(prev, dst, prev_off, prev_n);
+            prev = k, prev_off = off, prev_n = n;
             off += n;
         }
+        if (prev >= 0) drain(prev, dst, prev_off, prev_n);
     }
     void sync() { check(ofhe_hip_sync(ctx_, nullptr), "HipManager::sync"); }
     // ofhe_hip_finalize refuses (OFHE_ERR_STATE) while DeviceBuffers still
@@ -124,34 +142,62 @@ public:
     // them (they free through the context handle, not through this object),
     // and process exit reclaims it.
     ~HipManager() {
-        if (stage_) (void)ofhe_hip_host_free(ctx_, stage_);
+        for (int k = 0; k < 2; k++) {
+            if (ev_[k]) {
+                (void)ofhe_hip_event_sync(ev_[k]);
+                (void)ofhe_hip_event_destroy(ev_[k]);
+            }
+            if (stage_[k]) (void)ofhe_hip_host_free(ctx_, stage_[k]);
+        }
         if (ctx_) (void)ofhe_hip_finalize(ctx_);
     }
     HipManager(const HipManager&) = delete;
     HipManager& operator=(const HipManager&) = delete;
 
 private:
-    explicit HipManager(int device) : device_(device) { check(ofhe_hip_init(device, &ctx_), "HipManager"); }
-    // bytes the staging buffer takes per round (grown to the request, capped
+    explicit HipManager(int device) : device_(device) {
+        check(ofhe_hip_init(device, &ctx_), "HipManager");
+        for (int k = 0; k < 2; k++) check(ofhe_hip_event_create(ctx_, &ev_[k]), "HipManager staging event");
+    }
+    // bytes each staging buffer takes per round (grown to the request, capped
     // at kStageMax: larger copies go in rounds); caller holds stage_mu_
-    static constexpr size_t kStageMax = size_t(64) << 20;
+    static constexpr size_t kStageMax = size_t(32) << 20;
     size_t stage_room(size_t want) {
-        want = std::min(want, kStageMax);
+        want = std::min(std::max<size_t>(want, 1), kStageMax);
         if (stage_bytes_ < want) {
-            if (stage_) check(ofhe_hip_host_free(ctx_, stage_), "HipManager staging");
-            stage_ = nullptr;
-            stage_bytes_ = 0;
             size_t b = 4096;
             while (b < want) b <<= 1;
-            check(ofhe_hip_host_alloc(ctx_, b, &stage_), "HipManager staging");
+            for (int k = 0; k < 2; k++) {
+                stage_wait(k);  // a queued DMA may still read the old buffer
+                if (stage_[k]) check(ofhe_hip_host_free(ctx_, stage_[k]), "HipManager staging");
+                stage_[k] = nullptr;
+            }
+            stage_bytes_ = 0;
+            for (int k = 0; k < 2; k++) check(ofhe_hip_host_alloc(ctx_, b, &stage_[k]), "HipManager staging");
             stage_bytes_ = b;
         }
         return stage_bytes_;
     }
+    void stage_mark(int k) {
+        check(ofhe_hip_event_record(ev_[k], nullptr), "HipManager staging event");
+        pending_[k] = true;
+    }
+    void stage_wait(int k) {
+        if (!pending_[k]) return;
+        check(ofhe_hip_event_sync(ev_[k]), "HipManager staging event");
+        pending_[k] = false;
+    }
+    void drain(int k, void* dst, size_t off, size_t n) {
+        stage_wait(k);  // the DMA (and, in stream order, its producers) has finished
+        std::memcpy(static_cast<char*>(dst) + off, stage_[k], n);
+    }
     int device_;
     ofhe_ctx_t ctx_ = nullptr;
     std::mutex stage_mu_;
-    void* stage_ = nullptr;
+    void* stage_[2] = {nullptr, nullptr};
+    ofhe_event_t ev_[2] = {nullptr, nullptr};
+    bool pending_[2] = {false, false};
+    int next_ = 0;
     size_t stage_bytes_ = 0;
 };
 
@@ -553,7 +599,7 @@ public:
         if (!os) throw math_error("DCRTPolyHip::Save: stream write failed");
     }
     // The inverse of Save for `batch` consecutive records; every record must
-    // carry the same basis and format, and every value must be canonical.
+    // carry the same basis and format, and every value must be <= its modulus.
     static DCRTPolyHip Load(std::istream& is, uint32_t batch = 1, int device = 0) {
         if (batch == 0) throw deserialize_error("DCRTPolyHip::Load: batch must be >= 1");
         std::vector<uint64_t> flat, q0, r0;
@@ -577,8 +623,14 @@ public:
                 if (tq != m || trd != n || tco != 2 * n) throw deserialize_error("DCRTPolyHip::Load: tower params disagree");
                 if (t == 0) co = tco, f = tf;
                 if (tco != co || tf != f) throw deserialize_error("DCRTPolyHip::Load: towers of different rings / formats");
+                // NativeVectorT::load (mubintvecnat.h:684-702) takes the words as
+                // they are; the library itself writes the representative q (a
+                // negated zero of a coefficient-form AutomorphismTransform), so
+                // words <= m load unchanged and Save -> Load round-trips every
+                // library output.  Larger words are refused: the device kernels'
+                // lazy bounds assume inputs below 2q.
                 for (size_t i = off; i < off + n; i++)
-                    if (vals[i] >= m) throw deserialize_error("DCRTPolyHip::Load: value not below its modulus");
+                    if (vals[i] > m) throw deserialize_error("DCRTPolyHip::Load: value above its modulus");
                 q[t] = m;
                 r[t] = tr;
             }
@@ -749,6 +801,8 @@ public:
               "KeySwitchCore");
         return {std::move(o0), std::move(o1)};
     }
+
+    ofhe_ks_t handle() const { return h_; }
 
 private:
     ofhe_ks_t h_ = nullptr;

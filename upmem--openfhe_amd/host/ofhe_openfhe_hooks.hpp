@@ -15,6 +15,11 @@
 // Each hook gathers the towers into pinned staging memory, makes ONE launch
 // over every tower and scatters back (the host-buffer integration; the
 // resident integration keeps DCRTPolyHip objects instead, ofhe_dcrt.hpp).
+// Every hook is gated: it returns false, touching nothing, unless the device
+// (PCIe both ways included) beats the reference's own OpenMP loop over the
+// towers for this ring dimension and tower count -- the crossover measured by
+// tests/cpp/hook_crossover.cpp (profiles/r06_hook_crossover.txt)
+// -- and the caller then runs that loop unchanged.
 //
 //   DCRTPolyImpl::SwitchFormat          dcrtpoly-impl.h:2516-2523 -> if (!SwitchFormat(m_vectors)) <reference loop>
 //   DCRTPolyImpl::operator*= / Times    dcrtpoly.h:142-148, 185-200 -> TimesEq(m_vectors, rhs.m_vectors)
@@ -25,11 +30,16 @@
 //   DCRTPolyImpl::AutomorphismTransform dcrtpoly-impl.h:349-357     -> AutomorphismTransform(m_vectors, result.m_vectors, k)
 //   DCRTPolyImpl::Times / operator*= by scalar   dcrtpoly-impl.h:586-661 -> TimesScalarEq / TimesSignedEq
 //   DCRTPolyImpl::Minus by scalar       dcrtpoly-impl.h:565-584     -> MinusScalarEq
+//   KeySwitchHYBRID::KeySwitchCore      keyswitch-hybrid.cpp:324-328 -> KeySwitchCore(a, tag, ...)
+//     with the evaluation key made resident once by PutEvalKey (the
+//     EvalMultKeyGen / EvalAtIndexKeyGen hook, evalkeyrelin.h:136,166)
 #pragma once
 
 #include <algorithm>
 #include <cstdint>
 #include <map>
+#include <mutex>
+#include <string>
 #include <memory>
 #include <type_traits>
 #include <utility>
@@ -85,24 +95,116 @@ inline Staging& staging(int device, size_t words, int slot = 0) {
     return *s;
 }
 
-// Rings below this stay on the reference's CPU loop: binfhe's rings (N <= 2^11,
-// rgsw-acc-*.cpp) are launch-latency bound on the GPU and PCIe-bound through
-// the host-buffer hooks.
+// ---------------------------------------------------------------------------
+// The gate.  HookOp names a hook; the device takes a call when the ring
+// dimension n >= 2^min_log_n[op][tower class].  Tower classes are the tower
+// counts the crossover was measured at: T < 8 (T = 1), 8 <= T < 16, 16 <= T <
+// 48, T >= 48.  kNever keeps an op on the CPU loop at every measured size (the
+// element-wise hooks: at 24 PCIe bytes per coefficient the host-buffer path
+// cannot beat a host loop that streams the same words from DRAM; they pay
+// only in the resident integration, DCRTPolyHip).  Rings below kDeviceMinRing
+// (binfhe's, N <= 2^11, rgsw-acc-*.cpp) always stay on the CPU.
+// ---------------------------------------------------------------------------
+enum class HookOp : int {
+    SwitchFormat = 0,
+    TimesEq,
+    PlusEq,
+    MinusEq,
+    ApproxSwitchCRTBasis,
+    ApproxModUp,
+    ApproxModDown,
+    AutomorphismTransform,
+    ScalarEq,  // TimesScalarEq / TimesSignedEq / MinusScalarEq
+    KeySwitchCore,
+    Count
+};
+constexpr int kHookOps = (int)HookOp::Count;
+constexpr uint8_t kNever = 255, kAlways = 0;
 constexpr uint32_t kDeviceMinRing = 4096;
+
+inline const char* hook_name(HookOp op) {
+    static const char* names[kHookOps] = {"SwitchFormat",  "TimesEq",     "PlusEq",
+                                          "MinusEq",       "ApproxSwitchCRTBasis", "ApproxModUp",
+                                          "ApproxModDown", "AutomorphismTransform", "ScalarEq",
+                                          "KeySwitchCore"};
+    return names[(int)op];
+}
+inline int tower_class(size_t towers) { return towers < 8 ? 0 : towers < 16 ? 1 : towers < 48 ? 2 : 3; }
+
+struct Policy {
+    uint8_t min_log_n[kHookOps][4];
+    // PROVISIONAL (estimated from PCIe and CPU-loop rates; replaced by the
+    // table tests/cpp/hook_crossover.cpp prints on the MI355X box)
+    static Policy measured() {
+        Policy p{};
+        const uint8_t table[kHookOps][4] = {
+            /* SwitchFormat          */ {15, 13, 12, 12},
+            /* TimesEq               */ {kNever, kNever, kNever, kNever},
+            /* PlusEq                */ {kNever, kNever, kNever, kNever},
+            /* MinusEq               */ {kNever, kNever, kNever, kNever},
+            /* ApproxSwitchCRTBasis  */ {kNever, 15, 14, 13},
+            /* ApproxModUp           */ {15, 13, 12, 12},
+            /* ApproxModDown         */ {15, 13, 12, 12},
+            /* AutomorphismTransform */ {kNever, kNever, kNever, kNever},
+            /* ScalarEq              */ {kNever, kNever, kNever, kNever},
+            /* KeySwitchCore         */ {13, 12, 12, 12},
+        };
+        for (int o = 0; o < kHookOps; o++)
+            for (int c = 0; c < 4; c++) p.min_log_n[o][c] = table[o][c];
+        return p;
+    }
+    static Policy all(uint8_t v) {  // kAlways / kNever everywhere (tests, A/B timing)
+        Policy p{};
+        for (auto& r : p.min_log_n)
+            for (auto& c : r) c = v;
+        return p;
+    }
+};
+namespace detail {
+inline std::mutex& policy_mu() {
+    static std::mutex m;
+    return m;
+}
+inline Policy& policy_ref() {
+    static Policy p = Policy::measured();
+    return p;
+}
+}  // namespace detail
+inline Policy policy() {
+    std::lock_guard<std::mutex> lk(detail::policy_mu());
+    return detail::policy_ref();
+}
+inline void set_policy(const Policy& p) {
+    std::lock_guard<std::mutex> lk(detail::policy_mu());
+    detail::policy_ref() = p;
+}
+// Whether the device takes `op` on `towers` towers of ring dimension n.
+inline bool device_takes(HookOp op, uint32_t n, size_t towers) {
+    if (n < kDeviceMinRing || towers == 0) return false;
+    const uint8_t need = policy().min_log_n[(int)op][tower_class(towers)];
+    if (need == kNever) return false;
+    uint32_t lg = 0;
+    while ((1u << lg) < n) lg++;
+    return lg >= need;
+}
+template <class Towers>
+uint32_t ring_of(const Towers& towers) {
+    return towers.empty() ? 0 : (uint32_t)towers[0].GetParams()->GetRingDimension();
+}
 
 // Whether the device takes DCRTPolyImpl::SwitchFormat for these towers: a
 // power-of-two cyclotomic (PolyImpl::SwitchFormat sends rd != co / 2 to
-// ArbitrarySwitchFormat, poly-impl.h:412-420), ring dimension >= kDeviceMinRing,
-// every tower in the same format.
+// ArbitrarySwitchFormat, poly-impl.h:412-420), every tower in the same
+// format, and the gate.
 template <class Towers>
 bool device_switch_format(const Towers& towers) {
     if (towers.empty()) return false;
     const auto& p0 = *towers[0].GetParams();
     const uint32_t n = (uint32_t)p0.GetRingDimension();
-    if (n < kDeviceMinRing || (uint64_t)p0.GetCyclotomicOrder() != 2 * (uint64_t)n) return false;
+    if ((uint64_t)p0.GetCyclotomicOrder() != 2 * (uint64_t)n) return false;
     for (const auto& t : towers)
         if (t.GetFormat() != towers[0].GetFormat()) return false;
-    return true;
+    return device_takes(HookOp::SwitchFormat, n, towers.size());
 }
 
 // DCRTPolyImpl::SwitchFormat (dcrtpoly-impl.h:2516-2523): every tower
@@ -135,7 +237,9 @@ bool SwitchFormat(Towers& towers, int device = 0) {
 namespace detail {
 // a (op)= b over all towers in one launch; op 0 ModMul (Barrett), 1 ModAdd, 2 ModSub
 template <class Towers>
-void binary_eq(Towers& a, const Towers& b, int op, const char* what, int device) {
+bool binary_eq(Towers& a, const Towers& b, int op, const char* what, int device) {
+    const HookOp hop = op == 0 ? HookOp::TimesEq : op == 1 ? HookOp::PlusEq : HookOp::MinusEq;
+    if (!device_takes(hop, ring_of(a), a.size())) return false;
     TowerView va = view(a);
     TowerView vb = view(const_cast<Towers&>(b));
     if (va.q != vb.q || va.n != vb.n) throw math_error(std::string(what) + ": Modulus missmatch");
@@ -153,23 +257,26 @@ void binary_eq(Towers& a, const Towers& b, int op, const char* what, int device)
     check(rc, what);
     sa.download(words);
     sa.scatter(va.data, va.n);
+    return true;
 }
 }  // namespace detail
 
-// DCRTPolyImpl::operator*= (dcrtpoly.h:142-148; EVALUATION form, the caller checks)
+// DCRTPolyImpl::operator*= (dcrtpoly.h:142-148; EVALUATION form, the caller
+// checks).  Each returns false, touching nothing, when the gate keeps the op
+// on the caller's loop.
 template <class Towers>
-void TimesEq(Towers& a, const Towers& b, int device = 0) {
-    detail::binary_eq(a, b, 0, "hooks::TimesEq", device);
+bool TimesEq(Towers& a, const Towers& b, int device = 0) {
+    return detail::binary_eq(a, b, 0, "hooks::TimesEq", device);
 }
 // DCRTPolyImpl::operator+= (dcrtpoly-impl.h:410-416)
 template <class Towers>
-void PlusEq(Towers& a, const Towers& b, int device = 0) {
-    detail::binary_eq(a, b, 1, "hooks::PlusEq", device);
+bool PlusEq(Towers& a, const Towers& b, int device = 0) {
+    return detail::binary_eq(a, b, 1, "hooks::PlusEq", device);
 }
 // DCRTPolyImpl::operator-=
 template <class Towers>
-void MinusEq(Towers& a, const Towers& b, int device = 0) {
-    detail::binary_eq(a, b, 2, "hooks::MinusEq", device);
+bool MinusEq(Towers& a, const Towers& b, int device = 0) {
+    return detail::binary_eq(a, b, 2, "hooks::MinusEq", device);
 }
 
 // NTT plan over towers [t0, t0 + count) of a view (PlanCache: one per basis)
@@ -213,8 +320,9 @@ inline std::shared_ptr<ofhe_bconv_s> converter(int device, uint32_t log_n, const
 // QHatInvModq / QHatModp tables the pke layer precomputes
 // (rns-cryptoparameters.cpp:273-337; QHatModp row-major [sizeQ][sizeP]).
 template <class TowersQ, class TowersP>
-void ApproxSwitchCRTBasis(const TowersQ& x, TowersP& out, const std::vector<uint64_t>& QHatInvModq,
+bool ApproxSwitchCRTBasis(const TowersQ& x, TowersP& out, const std::vector<uint64_t>& QHatInvModq,
                           const std::vector<uint64_t>& QHatModp, int device = 0) {
+    if (!device_takes(HookOp::ApproxSwitchCRTBasis, ring_of(x), x.size() + out.size())) return false;
     TowerView vx = view(const_cast<TowersQ&>(x)), vo = view(out);
     if (vx.n != vo.n) throw math_error("hooks::ApproxSwitchCRTBasis: ring dimensions differ");
     auto bc = converter(device, vx.log_n, vx.q, vo.q, QHatInvModq, QHatModp, "hooks::ApproxSwitchCRTBasis");
@@ -226,6 +334,7 @@ void ApproxSwitchCRTBasis(const TowersQ& x, TowersP& out, const std::vector<uint
     check(ofhe_hip_approx_switch_crt_basis(bc.get(), sx.dev(), so.dev(), 1, nullptr), "hooks::ApproxSwitchCRTBasis");
     so.download(wo);
     so.scatter(vo.data, vo.n);
+    return true;
 }
 
 // DCRTPolyImpl::ApproxModUp (dcrtpoly-impl.h:1084-1131).  `towers` is
@@ -234,10 +343,13 @@ void ApproxSwitchCRTBasis(const TowersQ& x, TowersP& out, const std::vector<uint
 // values are ignored).  On return every tower holds ApproxModUp(x) in
 // EVALUATION form -- the Q towers x itself in evaluation form, the P towers
 // NTT(ApproxSwitchCRTBasis(x)) -- and says so (OverrideFormat), as the
-// reference's m_format = EVALUATION, m_params = paramsQP leave it.
+// reference's m_format = EVALUATION, m_params = paramsQP leave it.  The caller
+// appends the P towers only when device_takes(HookOp::ApproxModUp, n, sizeQ +
+// sizeP); a false return leaves `towers` untouched.
 template <class Towers>
-void ApproxModUp(Towers& towers, size_t sizeQ, const std::vector<uint64_t>& QHatInvModq,
+bool ApproxModUp(Towers& towers, size_t sizeQ, const std::vector<uint64_t>& QHatInvModq,
                  const std::vector<uint64_t>& QHatModp, int device = 0) {
+    if (!device_takes(HookOp::ApproxModUp, ring_of(towers), towers.size())) return false;
     using Fmt = std::decay_t<decltype(towers[0].GetFormat())>;
     if (sizeQ < 1 || sizeQ >= towers.size()) throw math_error("hooks::ApproxModUp: sizeQ outside (0, towers)");
     const bool eval = towers[0].GetFormat() == Fmt::EVALUATION;
@@ -258,6 +370,7 @@ void ApproxModUp(Towers& towers, size_t sizeQ, const std::vector<uint64_t>& QHat
     so.download(wo);
     so.scatter(v.data, v.n);
     for (auto& t : towers) t.OverrideFormat(Fmt::EVALUATION);
+    return true;
 }
 
 // DCRTPolyImpl::ApproxModDown (dcrtpoly-impl.h:1133-1175): x = the Q|P towers
@@ -268,9 +381,10 @@ void ApproxModUp(Towers& towers, size_t sizeQ, const std::vector<uint64_t>& QHat
 // t.ModInverse(p_j), bgvrns-cryptoparameters.cpp:83-88, derived here from t).
 // PHatInvModp / PHatModq ([sizeP][sizeQ]) as rns-cryptoparameters.cpp:172-215.
 template <class TowersQP, class TowersQ>
-void ApproxModDown(const TowersQP& x, TowersQ& out, const std::vector<uint64_t>& PInvModq,
+bool ApproxModDown(const TowersQP& x, TowersQ& out, const std::vector<uint64_t>& PInvModq,
                    const std::vector<uint64_t>& PHatInvModp, const std::vector<uint64_t>& PHatModq, uint64_t t = 0,
                    int device = 0) {
+    if (!device_takes(HookOp::ApproxModDown, ring_of(x), x.size())) return false;
     using Fmt = std::decay_t<decltype(x[0].GetFormat())>;
     for (const auto& tw : x)
         if (tw.GetFormat() != Fmt::EVALUATION) throw math_error("hooks::ApproxModDown: EVALUATION form expected");
@@ -295,6 +409,7 @@ void ApproxModDown(const TowersQP& x, TowersQ& out, const std::vector<uint64_t>&
     so.download(wo);
     so.scatter(vo.data, vo.n);
     for (auto& tw : out) tw.OverrideFormat(Fmt::EVALUATION);
+    return true;
 }
 
 // DCRTPolyImpl::AutomorphismTransform(k) (dcrtpoly-impl.h:349-357 ->
@@ -303,7 +418,8 @@ void ApproxModDown(const TowersQP& x, TowersQ& out, const std::vector<uint64_t>&
 // format (evaluation: bit-reversed slot permutation; coefficient: signed
 // permutation).  An even k throws math_error as the reference does.
 template <class Towers>
-void AutomorphismTransform(const Towers& x, Towers& out, uint32_t k, int device = 0) {
+bool AutomorphismTransform(const Towers& x, Towers& out, uint32_t k, int device = 0) {
+    if (!device_takes(HookOp::AutomorphismTransform, ring_of(x), x.size())) return false;
     using Fmt = std::decay_t<decltype(x[0].GetFormat())>;
     const bool eval = x[0].GetFormat() == Fmt::EVALUATION;
     for (const auto& tw : x)
@@ -321,12 +437,14 @@ void AutomorphismTransform(const Towers& x, Towers& out, uint32_t k, int device 
     so.download(words);
     so.scatter(vo.data, vo.n);
     for (auto& tw : out) tw.OverrideFormat(x[0].GetFormat());
+    return true;
 }
 
 namespace detail {
 // x_t (op)= s_t over all towers in one launch; op 0 ModMul (Shoup), 2 ModSub
 template <class Towers>
-void scalar_eq(Towers& x, const std::vector<uint64_t>& s, int op, const char* what, int device) {
+bool scalar_eq(Towers& x, const std::vector<uint64_t>& s, int op, const char* what, int device) {
+    if (!device_takes(HookOp::ScalarEq, ring_of(x), x.size())) return false;
     TowerView v = view(x);
     if (s.size() != v.q.size()) throw math_error(std::string(what) + ": one scalar per tower required");
     auto plan = plan_of(v, 0, v.q.size(), device);
@@ -339,6 +457,7 @@ void scalar_eq(Towers& x, const std::vector<uint64_t>& s, int op, const char* wh
           what);
     st.download(words);
     st.scatter(v.data, v.n);
+    return true;
 }
 }  // namespace detail
 
@@ -347,28 +466,148 @@ void scalar_eq(Towers& x, const std::vector<uint64_t>& s, int op, const char* wh
 // NativeVectorT::ModMul(Eq)(const IntegerType&), mubintvecnat.cpp:310-332):
 // tower t times s[t] mod q_t, in place (the caller copies first for Times).
 template <class Towers>
-void TimesScalarEq(Towers& x, const std::vector<uint64_t>& s, int device = 0) {
-    detail::scalar_eq(x, s, 0, "hooks::TimesScalarEq", device);
+bool TimesScalarEq(Towers& x, const std::vector<uint64_t>& s, int device = 0) {
+    return detail::scalar_eq(x, s, 0, "hooks::TimesScalarEq", device);
 }
 // DCRTPolyImpl::Times(NativeInteger::SignedNativeInt) (dcrtpoly-impl.h:597-605
 // -> PolyImpl::Times, poly-impl.h:237-252): a negative v multiplies by
 // q - (|v| mod q) in every tower.
 template <class Towers>
-void TimesSignedEq(Towers& x, int64_t v, int device = 0) {
+bool TimesSignedEq(Towers& x, int64_t v, int device = 0) {
+    if (!device_takes(HookOp::ScalarEq, ring_of(x), x.size())) return false;
     std::vector<uint64_t> s;
     for (auto& tw : x) {
         const uint64_t q = (uint64_t)tw.GetParams()->GetModulus().ConvertToInt();
         const uint64_t mag = v < 0 ? (uint64_t)0 - (uint64_t)v : (uint64_t)v;  // |v| without overflow at INT64_MIN
         s.push_back(v < 0 ? q - mag % q : mag);                              // q - 0 = q reduces to 0
     }
-    detail::scalar_eq(x, s, 0, "hooks::TimesSignedEq", device);
+    return detail::scalar_eq(x, s, 0, "hooks::TimesSignedEq", device);
 }
 // DCRTPolyImpl::Minus(const Integer&) / Minus(const std::vector<Integer>&)
 // (dcrtpoly-impl.h:565-584 -> PolyImpl::Minus, poly-impl.h:223-227): every word
 // of tower t minus s[t] mod q_t, in either format.
 template <class Towers>
-void MinusScalarEq(Towers& x, const std::vector<uint64_t>& s, int device = 0) {
-    detail::scalar_eq(x, s, 2, "hooks::MinusScalarEq", device);
+bool MinusScalarEq(Towers& x, const std::vector<uint64_t>& s, int device = 0) {
+    return detail::scalar_eq(x, s, 2, "hooks::MinusScalarEq", device);
+}
+
+// ---------------------------------------------------------------------------
+// HYBRID key switching, hooked one level up: KeySwitchHYBRID::KeySwitchCore
+// (keyswitch-hybrid.cpp:324-328) = EvalKeySwitchPrecomputeCore (digit
+// decomposition, per-digit ApproxSwitchCRTBasis, 330-412) ->
+// EvalFastKeySwitchCoreExt (key inner product, 438-482) -> two ApproxModDown
+// (414-435), all in one ofhe_hip_ks_core call on device-resident keys.
+// ---------------------------------------------------------------------------
+// One evaluation key on the device: EvalKeyRelinImpl's b and a vectors
+// (evalkeyrelin.h:136,166; numPartQ DCRTPolys over Q|P each) as two
+// DCRTPolyHip of batch numPartQ, with the bases they came with.
+struct HookEvalKey {
+    std::shared_ptr<DCRTParams> Q, P, QP;
+    uint32_t num_part_q = 0;
+    std::shared_ptr<const KeyCache::Key> key;
+};
+namespace detail {
+inline std::mutex& keys_mu() {
+    static std::mutex m;
+    return m;
+}
+inline std::map<std::string, std::shared_ptr<const HookEvalKey>>& keys() {
+    static std::map<std::string, std::shared_ptr<const HookEvalKey>> m;
+    return m;
+}
+}  // namespace detail
+
+// The EvalMultKeyGen / EvalAtIndexKeyGen side: uploads the key once, keyed by
+// its tag (Key::GetKeyTag).  bv[j] / av[j] are the tower vectors of
+// GetBVector()[j] / GetAVector()[j] (DCRTPolyImpl::GetAllElements,
+// dcrtpoly.h:391-397), all over the same Q|P basis in EVALUATION form, whose
+// last sizeP towers are P (CryptoParametersRNS::GetParamsP).
+template <class Towers>
+void PutEvalKey(const std::string& tag, const std::vector<const Towers*>& bv, const std::vector<const Towers*>& av,
+                size_t sizeP, int device = 0) {
+    if (bv.empty() || bv.size() != av.size()) throw math_error("hooks::PutEvalKey: b and a need numPartQ polynomials each");
+    TowerView v0 = view(const_cast<Towers&>(*bv[0]));
+    if (sizeP < 1 || sizeP >= v0.q.size()) throw math_error("hooks::PutEvalKey: sizeP outside (0, towers)");
+    const size_t T = v0.q.size(), n = v0.n, dnum = bv.size();
+    auto HK = std::make_shared<HookEvalKey>();
+    const size_t sizeQ = T - sizeP;
+    HK->Q = std::make_shared<DCRTParams>(2 * (uint32_t)n, std::vector<uint64_t>(v0.q.begin(), v0.q.begin() + sizeQ),
+                                         std::vector<uint64_t>(v0.psi.begin(), v0.psi.begin() + sizeQ), device);
+    HK->P = std::make_shared<DCRTParams>(2 * (uint32_t)n, std::vector<uint64_t>(v0.q.begin() + sizeQ, v0.q.end()),
+                                         std::vector<uint64_t>(v0.psi.begin() + sizeQ, v0.psi.end()), device);
+    HK->QP = std::make_shared<DCRTParams>(2 * (uint32_t)n, v0.q, v0.psi, device);
+    HK->num_part_q = (uint32_t)dnum;
+    std::vector<uint64_t> fb, fa;
+    fb.reserve(dnum * T * n);
+    fa.reserve(dnum * T * n);
+    for (size_t j = 0; j < dnum; j++) {
+        for (int which = 0; which < 2; which++) {
+            TowerView vj = view(const_cast<Towers&>(*(which ? av[j] : bv[j])));
+            if (vj.q != v0.q || vj.psi != v0.psi || vj.n != v0.n)
+                throw math_error("hooks::PutEvalKey: key polynomials over different bases");
+            auto& f = which ? fa : fb;
+            for (size_t t = 0; t < T; t++) f.insert(f.end(), vj.data[t], vj.data[t] + n);
+        }
+    }
+    DCRTPolyHip b(HK->QP, Format::EVALUATION, (uint32_t)dnum, DCRTPolyHip::Uninit{});
+    DCRTPolyHip a(HK->QP, Format::EVALUATION, (uint32_t)dnum, DCRTPolyHip::Uninit{});
+    b.SetValues(fb, Format::EVALUATION);
+    a.SetValues(fa, Format::EVALUATION);
+    HK->key = KeyCache::put("hooks:" + tag, std::move(b), std::move(a));
+    std::lock_guard<std::mutex> lk(detail::keys_mu());
+    detail::keys()[tag] = HK;
+}
+inline void EraseEvalKey(const std::string& tag) {
+    KeyCache::erase("hooks:" + tag);
+    std::lock_guard<std::mutex> lk(detail::keys_mu());
+    detail::keys().erase(tag);
+}
+inline std::shared_ptr<const HookEvalKey> GetEvalKey(const std::string& tag) {
+    std::lock_guard<std::mutex> lk(detail::keys_mu());
+    auto it = detail::keys().find(tag);
+    if (it == detail::keys().end()) throw math_error("hooks::KeySwitchCore: no resident evaluation key '" + tag + "'");
+    return it->second;
+}
+
+// KeySwitchCore(a, evalKey) for the key PutEvalKey stored under `tag`: a's
+// towers (Ql, a prefix of Q, EVALUATION form) -> ct0, ct1 (the caller's two
+// DCRTPoly(paramsQl, EVALUATION) outputs, l towers each), t = the BGV
+// plaintext modulus or 0 (cryptoParams->GetNoiseScale() == 1, 313).  Gather
+// a, one upload, one ofhe_hip_ks_core, one download of both outputs, scatter.
+// Returns false, touching nothing, when the gate keeps it on the CPU.
+template <class TowersQl, class TowersOut>
+bool KeySwitchCore(const TowersQl& a, const std::string& tag, uint64_t t, TowersOut& ct0, TowersOut& ct1,
+                   int device = 0) {
+    auto HK = GetEvalKey(tag);
+    const size_t T = HK->QP->Towers();
+    if (!device_takes(HookOp::KeySwitchCore, ring_of(a), T)) return false;
+    using Fmt = std::decay_t<decltype(a[0].GetFormat())>;
+    for (const auto& tw : a)
+        if (tw.GetFormat() != Fmt::EVALUATION) throw math_error("hooks::KeySwitchCore: EVALUATION form expected");
+    TowerView va = view(const_cast<TowersQl&>(a)), v0 = view(ct0), v1 = view(ct1);
+    const size_t l = va.q.size(), n = va.n;
+    const auto& Qm = HK->Q->Moduli();
+    if (n != HK->QP->GetRingDimension()) throw math_error("hooks::KeySwitchCore: ring dimension differs from the key's");
+    if (l > Qm.size() || !std::equal(va.q.begin(), va.q.end(), Qm.begin()))
+        throw math_error("hooks::KeySwitchCore: ciphertext basis is not a prefix of the key's Q");
+    if (v0.q != va.q || v1.q != va.q || v0.n != n || v1.n != n)
+        throw math_error("hooks::KeySwitchCore: outputs must be over the ciphertext's basis");
+    auto ks = KsCache::get(*HK->Q, *HK->P, HK->num_part_q);
+    const size_t words = l * n;
+    Staging& sx = staging(device, words, 0);
+    Staging& so = staging(device, 2 * words, 1);
+    sx.gather(cptr(va.data), n);
+    sx.upload(words);
+    check(ofhe_hip_ks_core(ks->handle(), (uint32_t)l, sx.dev(), HK->key->b.data(), HK->key->a.data(), so.dev(),
+                           so.dev() + words, t, 1, nullptr),
+          "hooks::KeySwitchCore");
+    so.download(2 * words);
+    std::vector<uint64_t*> both(v0.data);
+    both.insert(both.end(), v1.data.begin(), v1.data.end());
+    so.scatter(both, n);
+    for (auto& tw : ct0) tw.OverrideFormat(Fmt::EVALUATION);
+    for (auto& tw : ct1) tw.OverrideFormat(Fmt::EVALUATION);
+    return true;
 }
 
 }  // namespace hooks

@@ -60,6 +60,10 @@ _SIGS = {
     "ofhe_hip_copy_to_host": (ctypes.c_int, [_vp, _vp, _vp, ctypes.c_size_t, _vp]),
     "ofhe_hip_copy_device": (ctypes.c_int, [_vp, _vp, _vp, ctypes.c_size_t, _vp]),
     "ofhe_hip_sync": (ctypes.c_int, [_vp, _vp]),
+    "ofhe_hip_event_create": (ctypes.c_int, [_vp, ctypes.POINTER(_vp)]),
+    "ofhe_hip_event_record": (ctypes.c_int, [_vp, _vp]),
+    "ofhe_hip_event_sync": (ctypes.c_int, [_vp]),
+    "ofhe_hip_event_destroy": (ctypes.c_int, [_vp]),
     "ofhe_hip_trim": (ctypes.c_int, [_vp, ctypes.c_size_t]),
     "ofhe_hip_plan_create": (ctypes.c_int, [_vp, ctypes.c_uint32, ctypes.c_uint32, _u64p, _u64p,
                                             ctypes.POINTER(_vp)]),

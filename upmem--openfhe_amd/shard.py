@@ -108,7 +108,10 @@ def key_broadcaster(ctx, rank: int, world: int):
     The ranks agree on the backend: each reports whether its communicator
     came up (all_reduce MIN of an ok flag), and unless every rank succeeded
     they all close theirs and use torch.distributed -- a rank never calls
-    ncclBroadcast while a peer sits in dist.broadcast."""
+    ncclBroadcast while a peer sits in dist.broadcast.  Every rank's own
+    outcome (communicator up or the error it raised) is gathered onto the
+    returned function as `.per_rank`, one {"rank", "comm", "error"} per rank,
+    so a fallback names the rank that caused it."""
     import torch
     import torch.distributed as dist
 
@@ -125,12 +128,18 @@ def key_broadcaster(ctx, rank: int, world: int):
     dev = torch.device("cuda", torch.cuda.current_device()) if backend == "nccl" else torch.device("cpu")
     ok = torch.tensor([1 if comm is not None else 0], dtype=torch.int32, device=dev)
     dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+    per_rank = [None] * dist.get_world_size()
+    dist.all_gather_object(per_rank, {"rank": rank, "comm": comm is not None, "error": err})
     if int(ok.item()) == 1:
-        return (lambda key, src=0: bcast_evalkey_capi(comm, key, src)), "ofhe_hip_bcast_evalkey (RCCL)", comm
+        fn = lambda key, src=0: bcast_evalkey_capi(comm, key, src)  # noqa: E731
+        fn.per_rank = per_rank
+        return fn, "ofhe_hip_bcast_evalkey (RCCL)", comm
     if comm is not None:
         comm.close()
     why = err if err else "a peer rank's C-ABI communicator failed"
-    return (lambda key, src=0: broadcast_evalkey(key, src)), f"torch.distributed {backend} (C-ABI comm: {why})", None
+    fn = lambda key, src=0: broadcast_evalkey(key, src)  # noqa: E731
+    fn.per_rank = per_rank
+    return fn, f"torch.distributed {backend} (C-ABI comm: {why})", None
 
 
 def max_over_ranks(value: float, device=None) -> float:
