@@ -10,7 +10,7 @@
 //
 // Prints one line per (op, N, T): median ms of each leg, then the table the
 // gate takes: per op and tower class the smallest log N from which the device
-// wins at every measured N up to 2^max, else kNever.
+// wins (by kMargin) at every measured N up to 2^max, else kNever.
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -25,6 +25,9 @@ using mock::Format;
 using mock::Towers;
 using ofhe::hooks::HookOp;
 using Clock = std::chrono::steady_clock;
+// the device must beat the CPU loop by this factor for the gate to take it
+// (run-to-run noise of either leg is a few per cent)
+constexpr double kMargin = 1.10;
 
 // median of reps (>= 3, until ~budget seconds) of fn in ms
 static double time_ms(const std::function<void()>& fn, double budget = 0.25) {
@@ -108,7 +111,7 @@ int main(int argc, char** argv) {
                 const double dev = time_ms(cs.fn);
                 ofhe::hooks::set_policy(ofhe::hooks::Policy::all(ofhe::hooks::kNever));
                 const double cpu = time_ms(cs.fn);
-                wins[(int)cs.op][c][lg] = dev < cpu;
+                wins[(int)cs.op][c][lg] = cpu >= kMargin * dev;
                 std::printf("  %-22s %6u %4zu %11.3f %11.3f %7.2f\n", ofhe::hooks::hook_name(cs.op), lg, T, dev, cpu,
                             cpu / dev);
                 std::fflush(stdout);

@@ -15,7 +15,10 @@ forward stages and first 8 inverse stages on every 256-element group equal
 The reference loops are transformnat-impl.h:300-354 (forward) and 492-552
 (inverse), restated in oracle/transform_py.py.
 
-  python tools/mma_model.py
+  python tools/mma_model.py            the identities above (exact integers)
+  python tools/mma_model.py --budget   round 6's instruction / issue model of
+                                       the whole pipeline on the matrix cores
+                                       (DESIGN.md (f), "The 0.40 target")
 """
 import os
 import sys
@@ -126,5 +129,73 @@ def main():
     print("inverse block stages as F' + twiddle + F' + twist, then GS column stages:", a == x)
 
 
+# ---------------------------------------------------------------------------
+# Round 6: the pipeline-wide matrix-core budget.  Inputs are measurements,
+# each with its record:
+#   * k_block (butterflies), k_tcols fwd / inv: SQ_INSTS_VALU per coefficient,
+#     profiles/pmc_current.json (r05y, the shipped build): 180.75 / 80.1 / 95.1
+#   * k_block_m16 (round 3, 4 MFMA rounds): 172.0 per coefficient measured
+#     (profiles/r03_block_m16_pmc/), issue 0.121 wave-instr per SIMD-cycle;
+#     its loop body, recompiled from 2ae2740 (ntt_m16.hpp) and counted by
+#     instruction: 1235 VALU per 8 coefficients per lane = 154.4 per
+#     coefficient, plus 152 static instructions once per 16 coefficients
+#     (setup: fragment staging, constants, addresses) = 9.5
+#   * the m16 header's model: 4 x (digit split 3 + reduce 12) + 4 Shoup x 14 +
+#     Montgomery Hadamard 20 = 136
+# A matrix-core radix-16 round, measured: the m16 loop minus its non-round
+# work (twist, two twiddles, inverse twist: 4 Shoup x 14; Montgomery
+# Hadamard 20) over its four rounds.
+# ---------------------------------------------------------------------------
+M16_LOOP = 1235 / 8          # VALU per coefficient in k_block_m16's loop
+M16_SETUP = 152 / 16         # once-per-thread part
+M16_MEASURED = 172.0
+SHOUP, MONT = 14, 20
+ROUND_MMA = (M16_LOOP - 4 * SHOUP - MONT) / 4
+BUTTERFLY = {"colpass<fwd>": 80.1, "k_block<fused>": 180.75, "colpass<inv>": 95.1}
+SHIPPED = sum(BUTTERFLY.values())
+HEADLINE = 8.17e10           # BENCH_r05 coefficients/s (the driver's record)
+ISSUE_MEASURED_M16 = 0.121   # k_block_m16's VALU issue per SIMD-cycle
+ISSUE_BUTTERFLY = 0.245
+
+
+def budget():
+    # The column passes' two radix-16 rounds are shared 16 x 16 maps with the
+    # twiddles folded in (round 1: one matrix per tower; round 2: 16, by the
+    # row block, transformnat-impl.h:305-311): two MMA rounds and no twist.
+    # I/O: loads, stores, canonicalisation of the inverse output (~6), and the
+    # per-thread setup as m16's.
+    col = 2 * ROUND_MMA + 6 + M16_SETUP
+    rows = [
+        ("butterflies (shipped)", BUTTERFLY["colpass<fwd>"], BUTTERFLY["k_block<fused>"], BUTTERFLY["colpass<inv>"]),
+        ("MMA column passes + butterfly block", col, BUTTERFLY["k_block<fused>"], col),
+        ("MMA column passes + k_block_m16", col, M16_MEASURED, col),
+        ("MMA everywhere, no per-thread setup", 2 * ROUND_MMA + 6, M16_LOOP, 2 * ROUND_MMA + 6),
+    ]
+    print(f"matrix-core radix-16 round, measured: {ROUND_MMA:.1f} VALU per coefficient "
+          f"(m16 loop {M16_LOOP:.1f} - 4 Shoup x {SHOUP} - Hadamard {MONT}, over 4 rounds)")
+    print(f"m16 header model 136 vs measured {M16_MEASURED}: loop {M16_LOOP:.1f} + setup {M16_SETUP:.1f} "
+          f"= {M16_LOOP + M16_SETUP:.1f}; the loop's v_mov_b32 alone is {189 / 8:.1f} per coefficient")
+    print(f"{'variant':42s} {'fwd col':>8s} {'block':>8s} {'inv col':>8s} {'total':>8s} "
+          f"{'@0.245':>9s} {'@0.121':>9s}")
+    for name, a, b, c in rows:
+        tot = a + b + c
+        # throughput at the shipped issue rate (VALU-bound, same clock), and at m16's measured issue
+        at_shipped = HEADLINE * SHIPPED / tot
+        at_m16 = at_shipped * ISSUE_MEASURED_M16 / ISSUE_BUTTERFLY
+        print(f"{name:42s} {a:8.1f} {b:8.1f} {c:8.1f} {tot:8.1f} {at_shipped / 3.33e11:9.3f} {at_m16 / 3.33e11:9.3f}")
+    # matrix-pipe share in a column pass at full overlap: 16 v_mfma_i32_32x32x32_i8
+    # per 512 elements per round (32 cycles each at the dense int8 peak) against
+    # the round's VALU at 4 cycles per wave64 instruction
+    mfma_cyc = 16 * 32 / 512
+    valu_cyc = ROUND_MMA * 4 / 64
+    print(f"column-pass round per coefficient per SIMD: matrix pipe {mfma_cyc:.2f} cycles, VALU {valu_cyc:.2f} "
+          f"-> matrix pipe {mfma_cyc / max(mfma_cyc, valu_cyc):.0%} busy at full overlap")
+    print("columns @0.245 / @0.121: fraction of the 8 TB/s HBM roofline (24 B/coeff) at the shipped issue rate "
+          "and at the matrix-core kernel's measured one; the north star asks >= 0.40")
+
+
 if __name__ == "__main__":
-    main()
+    if "--budget" in sys.argv:
+        budget()
+    else:
+        main()

@@ -303,12 +303,15 @@ public:
         void* h = nullptr;
         check(ofhe_hip_host_alloc(m_->ctx(), words * sizeof(uint64_t), &h), "Staging");
         host_ = static_cast<uint64_t*>(h);
+        for (auto& e : ev_) check(ofhe_hip_event_create(m_->ctx(), &e), "Staging");
     }
     ~Staging() {
         if (host_) {
             (void)ofhe_hip_sync(m_->ctx(), nullptr);
             (void)ofhe_hip_host_free(m_->ctx(), host_);
         }
+        for (auto& e : ev_)
+            if (e) (void)ofhe_hip_event_destroy(e);
     }
     Staging(const Staging&) = delete;
     Staging& operator=(const Staging&) = delete;
@@ -334,11 +337,61 @@ public:
         m_->sync();
     }
 
+    // gather + upload, pipelined: towers go in chunks of ~kChunkBytes, each
+    // chunk's host copies (one tower per OpenMP thread when the caller builds
+    // with OpenMP, as OpenFHE does) run while the previous chunk's DMA is in
+    // flight.  Chunks land in disjoint parts of the pinned buffer, and every
+    // hook ends in get_towers' wait, so no chunk overwrites a buffer a DMA
+    // still reads.  Tower t lands at word t * n of the device buffer.
+    void put_towers(const std::vector<const uint64_t*>& towers, size_t n) {
+        if (towers.size() * n > n_) throw math_error("Staging::put_towers: more words than the buffer holds");
+        const size_t per = chunk_towers(n), T = towers.size();
+        for (size_t t0 = 0; t0 < T; t0 += per) {
+            const size_t t1 = std::min(T, t0 + per);
+            copy_towers(t0, t1, [&](size_t t) { std::memcpy(host_ + t * n, towers[t], n * 8); });
+            check(ofhe_hip_copy_to_device(m_->ctx(), dev() + t0 * n, host_ + t0 * n, (t1 - t0) * n * 8, nullptr),
+                  "Staging::put_towers");
+        }
+    }
+    // download + scatter, pipelined the other way: every chunk's DMA is
+    // queued (in stream order, after the launch that produces it), and chunk
+    // k is scattered once its event fires while chunk k + 1 is in flight.
+    // Returns with every word in place (the reference's synchronous
+    // copy_from_pim, PimManager.cpp:39-54).
+    void get_towers(const std::vector<uint64_t*>& towers, size_t n) {
+        if (towers.size() * n > n_) throw math_error("Staging::get_towers: more words than the buffer holds");
+        const size_t per = chunk_towers(n), T = towers.size();
+        size_t prev0 = 0, prev1 = 0, k = 0;
+        auto scatter_chunk = [&](size_t a, size_t b, int e) {
+            check(ofhe_hip_event_sync(ev_[e]), "Staging::get_towers");
+            copy_towers(a, b, [&](size_t t) { std::memcpy(towers[t], host_ + t * n, n * 8); });
+        };
+        for (size_t t0 = 0; t0 < T; t0 += per, k++) {
+            const size_t t1 = std::min(T, t0 + per);
+            check(ofhe_hip_copy_to_host(m_->ctx(), host_ + t0 * n, dev() + t0 * n, (t1 - t0) * n * 8, nullptr),
+                  "Staging::get_towers");
+            check(ofhe_hip_event_record(ev_[k & 1], nullptr), "Staging::get_towers");
+            if (k) scatter_chunk(prev0, prev1, (int)((k - 1) & 1));
+            prev0 = t0, prev1 = t1;
+        }
+        if (k) scatter_chunk(prev0, prev1, (int)((k - 1) & 1));
+    }
+
 private:
+    static constexpr size_t kChunkBytes = size_t(8) << 20;
+    static size_t chunk_towers(size_t n) { return std::max<size_t>(1, kChunkBytes / (n * 8)); }
+    template <class F>
+    static void copy_towers(size_t t0, size_t t1, F f) {
+#ifdef _OPENMP
+#pragma omp parallel for schedule(static) if (t1 - t0 > 1)
+#endif
+        for (size_t t = t0; t < t1; t++) f(t);
+    }
     HipManager* m_;
     DeviceBuffer dev_;
     size_t n_;
     uint64_t* host_ = nullptr;
+    ofhe_event_t ev_[2] = {nullptr, nullptr};
 };
 
 // ---------------------------------------------------------------------------

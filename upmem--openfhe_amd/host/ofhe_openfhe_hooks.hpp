@@ -133,21 +133,23 @@ inline int tower_class(size_t towers) { return towers < 8 ? 0 : towers < 16 ? 1 
 
 struct Policy {
     uint8_t min_log_n[kHookOps][4];
-    // PROVISIONAL (estimated from PCIe and CPU-loop rates; replaced by the
-    // table tests/cpp/hook_crossover.cpp prints on the MI355X box)
+    // measured: tests/cpp/hook_crossover.cpp on the MI355X box (host
+    // buffers, pipelined pinned staging, both PCIe directions; the CPU loop
+    // on 16 OpenMP threads), device taken where it wins by >= 10 % at that
+    // N and every larger one (profiles/r06_hook_crossover.txt)
     static Policy measured() {
         Policy p{};
         const uint8_t table[kHookOps][4] = {
-            /* SwitchFormat          */ {15, 13, 12, 12},
-            /* TimesEq               */ {kNever, kNever, kNever, kNever},
+            /* SwitchFormat          */ {13, 13, 14, 13},
+            /* TimesEq               */ {16, kNever, kNever, kNever},
             /* PlusEq                */ {kNever, kNever, kNever, kNever},
             /* MinusEq               */ {kNever, kNever, kNever, kNever},
-            /* ApproxSwitchCRTBasis  */ {kNever, 15, 14, 13},
-            /* ApproxModUp           */ {15, 13, 12, 12},
-            /* ApproxModDown         */ {15, 13, 12, 12},
-            /* AutomorphismTransform */ {kNever, kNever, kNever, kNever},
+            /* ApproxSwitchCRTBasis  */ {17, 13, 12, 12},
+            /* ApproxModUp           */ {14, 12, 12, 12},
+            /* ApproxModDown         */ {12, 12, 12, 12},
+            /* AutomorphismTransform */ {13, 13, 14, 14},
             /* ScalarEq              */ {kNever, kNever, kNever, kNever},
-            /* KeySwitchCore         */ {13, 12, 12, 12},
+            /* KeySwitchCore         */ {12, 12, 12, 12},
         };
         for (int o = 0; o < kHookOps; o++)
             for (int c = 0; c < 4; c++) p.min_log_n[o][c] = table[o][c];
@@ -223,13 +225,11 @@ bool SwitchFormat(Towers& towers, int device = 0) {
     auto plan = PlanCache::get(device, v.log_n, v.q, v.psi);
     const size_t words = v.q.size() * (size_t)v.n;
     Staging& st = staging(device, words);
-    st.gather(cptr(v.data), v.n);
-    st.upload(words);
+    st.put_towers(cptr(v.data), v.n);
     check(to_eval ? ofhe_hip_ntt_fwd(plan->get(), st.dev(), 1, nullptr)
                   : ofhe_hip_ntt_inv(plan->get(), st.dev(), 1, nullptr),
           "hooks::SwitchFormat");
-    st.download(words);
-    st.scatter(v.data, v.n);
+    st.get_towers(v.data, v.n);
     for (auto& t : towers) t.OverrideFormat(to_eval ? Fmt::EVALUATION : Fmt::COEFFICIENT);
     return true;
 }
@@ -247,16 +247,13 @@ bool binary_eq(Towers& a, const Towers& b, int op, const char* what, int device)
     const size_t words = va.q.size() * (size_t)va.n;
     Staging& sa = staging(device, words, 0);
     Staging& sb = staging(device, words, 1);
-    sa.gather(cptr(va.data), va.n);
-    sb.gather(cptr(vb.data), vb.n);
-    sa.upload(words);
-    sb.upload(words);
+    sa.put_towers(cptr(va.data), va.n);
+    sb.put_towers(cptr(vb.data), vb.n);
     int rc = op == 0   ? ofhe_hip_modmul_vv(plan->get(), sa.dev(), sb.dev(), sa.dev(), 1, nullptr)
              : op == 1 ? ofhe_hip_modadd_vv(plan->get(), sa.dev(), sb.dev(), sa.dev(), 1, nullptr)
                        : ofhe_hip_modsub_vv(plan->get(), sa.dev(), sb.dev(), sa.dev(), 1, nullptr);
     check(rc, what);
-    sa.download(words);
-    sa.scatter(va.data, va.n);
+    sa.get_towers(va.data, va.n);
     return true;
 }
 }  // namespace detail
@@ -329,11 +326,9 @@ bool ApproxSwitchCRTBasis(const TowersQ& x, TowersP& out, const std::vector<uint
     const size_t wx = vx.q.size() * (size_t)vx.n, wo = vo.q.size() * (size_t)vo.n;
     Staging& sx = staging(device, wx, 0);
     Staging& so = staging(device, wo, 1);
-    sx.gather(cptr(vx.data), vx.n);
-    sx.upload(wx);
+    sx.put_towers(cptr(vx.data), vx.n);
     check(ofhe_hip_approx_switch_crt_basis(bc.get(), sx.dev(), so.dev(), 1, nullptr), "hooks::ApproxSwitchCRTBasis");
-    so.download(wo);
-    so.scatter(vo.data, vo.n);
+    so.get_towers(vo.data, vo.n);
     return true;
 }
 
@@ -363,12 +358,10 @@ bool ApproxModUp(Towers& towers, size_t sizeQ, const std::vector<uint64_t>& QHat
     const size_t wx = sizeQ * (size_t)v.n, wo = v.q.size() * (size_t)v.n;
     Staging& sx = staging(device, wx, 0);
     Staging& so = staging(device, wo, 1);
-    sx.gather(cptr(std::vector<uint64_t*>(v.data.begin(), v.data.begin() + sizeQ)), v.n);
-    sx.upload(wx);
+    sx.put_towers(cptr(std::vector<uint64_t*>(v.data.begin(), v.data.begin() + sizeQ)), v.n);
     check(ofhe_hip_approx_mod_up(pq->get(), pp->get(), bc.get(), eval ? 1 : 0, sx.dev(), so.dev(), 1, nullptr),
           "hooks::ApproxModUp");
-    so.download(wo);
-    so.scatter(v.data, v.n);
+    so.get_towers(v.data, v.n);
     for (auto& t : towers) t.OverrideFormat(Fmt::EVALUATION);
     return true;
 }
@@ -401,13 +394,11 @@ bool ApproxModDown(const TowersQP& x, TowersQ& out, const std::vector<uint64_t>&
     const size_t wx = vx.q.size() * (size_t)vx.n, wo = sizeQ * (size_t)vx.n;
     Staging& sx = staging(device, wx, 0);
     Staging& so = staging(device, wo, 1);
-    sx.gather(cptr(vx.data), vx.n);
-    sx.upload(wx);
+    sx.put_towers(cptr(vx.data), vx.n);
     check(ofhe_hip_approx_mod_down(pq->get(), pp->get(), bc.get(), PInvModq.data(), t, sx.dev(), so.dev(), 1,
                                    nullptr),
           "hooks::ApproxModDown");
-    so.download(wo);
-    so.scatter(vo.data, vo.n);
+    so.get_towers(vo.data, vo.n);
     for (auto& tw : out) tw.OverrideFormat(Fmt::EVALUATION);
     return true;
 }
@@ -430,12 +421,10 @@ bool AutomorphismTransform(const Towers& x, Towers& out, uint32_t k, int device 
     const size_t words = vx.q.size() * (size_t)vx.n;
     Staging& sx = staging(device, words, 0);
     Staging& so = staging(device, words, 1);
-    sx.gather(cptr(vx.data), vx.n);
-    sx.upload(words);
+    sx.put_towers(cptr(vx.data), vx.n);
     check(ofhe_hip_automorphism(plan->get(), k, eval ? 1 : 0, sx.dev(), so.dev(), 1, nullptr),
           "hooks::AutomorphismTransform");
-    so.download(words);
-    so.scatter(vo.data, vo.n);
+    so.get_towers(vo.data, vo.n);
     for (auto& tw : out) tw.OverrideFormat(x[0].GetFormat());
     return true;
 }
@@ -450,13 +439,11 @@ bool scalar_eq(Towers& x, const std::vector<uint64_t>& s, int op, const char* wh
     auto plan = plan_of(v, 0, v.q.size(), device);
     const size_t words = v.q.size() * (size_t)v.n;
     Staging& st = staging(device, words, 0);
-    st.gather(cptr(v.data), v.n);
-    st.upload(words);
+    st.put_towers(cptr(v.data), v.n);
     check(op == 0 ? ofhe_hip_modmul_scalar(plan->get(), st.dev(), s.data(), st.dev(), 1, nullptr)
                   : ofhe_hip_modsub_scalar(plan->get(), st.dev(), s.data(), st.dev(), 1, nullptr),
           what);
-    st.download(words);
-    st.scatter(v.data, v.n);
+    st.get_towers(v.data, v.n);
     return true;
 }
 }  // namespace detail
@@ -596,15 +583,13 @@ bool KeySwitchCore(const TowersQl& a, const std::string& tag, uint64_t t, Towers
     const size_t words = l * n;
     Staging& sx = staging(device, words, 0);
     Staging& so = staging(device, 2 * words, 1);
-    sx.gather(cptr(va.data), n);
-    sx.upload(words);
+    sx.put_towers(cptr(va.data), n);
     check(ofhe_hip_ks_core(ks->handle(), (uint32_t)l, sx.dev(), HK->key->b.data(), HK->key->a.data(), so.dev(),
                            so.dev() + words, t, 1, nullptr),
           "hooks::KeySwitchCore");
-    so.download(2 * words);
     std::vector<uint64_t*> both(v0.data);
     both.insert(both.end(), v1.data.begin(), v1.data.end());
-    so.scatter(both, n);
+    so.get_towers(both, n);
     for (auto& tw : ct0) tw.OverrideFormat(Fmt::EVALUATION);
     for (auto& tw : ct1) tw.OverrideFormat(Fmt::EVALUATION);
     return true;
