@@ -716,6 +716,75 @@ static void register_tests() {
         EXPECT_EQ(ok, true, "staged transform equals SwitchFormat");
         EXPECT_THROW(st.gather(std::vector<const uint64_t*>(5, src[0]), n), math_error, "gather overflow");
     });
+    // Staging::put_towers / get_towers (round 6, the hooks' path): towers in
+    // ~8 MiB chunks, host copies overlapping the previous chunk's DMA, results
+    // back behind per-chunk events.  N = 2^17 (1 MiB per tower) x 19 towers is
+    // three chunks, the last one partial; the staged forward transform equals
+    // SwitchFormat on a resident copy, and a second round trip through the same
+    // (reused) staging slot sees the new words, not the first call's.
+    TEST("Staging.put_get_towers_chunked", [] {
+        const uint32_t m = 1u << 18, n = m / 2, T = 19;
+        std::vector<uint64_t> q;
+        uint64_t x = first_prime(60, m);
+        for (uint32_t t = 0; t < T; t++) q.push_back(x = previous_prime(x, m));
+        auto P = params(m, q);
+        std::mt19937_64 rng(23);
+        Staging st(P->manager(), (size_t)T * n);
+        for (int round = 0; round < 2; round++) {
+            std::vector<std::vector<uint64_t>> towers(T, std::vector<uint64_t>(n));
+            std::vector<uint64_t> flat;
+            for (uint32_t t = 0; t < T; t++)
+                for (auto& v : towers[t]) flat.push_back(v = rng() % q[t]);
+            std::vector<const uint64_t*> src;
+            std::vector<uint64_t*> dst;
+            for (auto& tv : towers) src.push_back(tv.data()), dst.push_back(tv.data());
+            st.put_towers(src, n);
+            ofhe::check(ofhe_hip_ntt_fwd(P->plan(), st.dev(), 1, nullptr), "ntt_fwd");
+            st.get_towers(dst, n);
+            DCRTPolyHip ref(P, Format::COEFFICIENT);
+            ref.SetValues(flat, Format::COEFFICIENT);
+            ref.SwitchFormat();
+            auto want = ref.GetValues();
+            size_t bad = 0;
+            for (uint32_t t = 0; t < T; t++)
+                for (uint32_t i = 0; i < n; i++) bad += towers[t][i] != want[(size_t)t * n + i];
+            EXPECT_EQ(bad, (size_t)0, round ? "second round trip (reused slot)" : "chunked staged transform");
+        }
+        EXPECT_THROW(st.put_towers(std::vector<const uint64_t*>(T + 1, nullptr), n), math_error, "put overflow");
+    });
+    // HipManager's event-ordered copies (round 6): a copy larger than one
+    // staging round (32 MiB) alternates the two pinned buffers; back-to-back
+    // uploads into the same buffer, each followed by a launch that reads it,
+    // see their own words (the DMA is ordered after the queued launch, the
+    // staging buffer is refilled only after its event).
+    TEST("HipManager.event_ordered_copies", [] {
+        const uint32_t m = 1u << 18, n = m / 2, T = 40;  // 42 MB: two staging rounds
+        std::vector<uint64_t> q;
+        uint64_t x = first_prime(60, m);
+        for (uint32_t t = 0; t < T; t++) q.push_back(x = previous_prime(x, m));
+        auto P = params(m, q);
+        std::mt19937_64 rng(29);
+        std::vector<uint64_t> a((size_t)T * n), b(a.size());
+        for (size_t i = 0; i < a.size(); i++) a[i] = rng() % q[i / n], b[i] = rng() % q[i / n];
+        DCRTPolyHip X(P, Format::EVALUATION), Y(P, Format::EVALUATION);
+        X.SetValues(a, Format::EVALUATION);
+        EXPECT_EQ(X.GetValues() == a, true, "two-round upload / download");
+        // Y = a, then S1 = X + Y queued, then Y = b (same buffer) and S2 = X + Y
+        Y.SetValues(a, Format::EVALUATION);
+        DCRTPolyHip S1 = X + Y;
+        Y.SetValues(b, Format::EVALUATION);
+        DCRTPolyHip S2 = X + Y;
+        const auto s1 = S1.GetValues(), s2 = S2.GetValues();
+        size_t bad1 = 0, bad2 = 0;
+        for (size_t i = 0; i < a.size(); i++) {
+            const uint64_t qi = q[i / n];
+            const uint64_t w1 = (a[i] + a[i]) % qi, w2 = (a[i] + b[i]) % qi;
+            bad1 += s1[i] != w1;
+            bad2 += s2[i] != w2;
+        }
+        EXPECT_EQ(bad1, (size_t)0, "the launch queued before the re-upload read the first words");
+        EXPECT_EQ(bad2, (size_t)0, "the launch after it reads the second");
+    });
     // KsCache / KeyCache: one key-switch engine per parameter set, keys resident
     // by id; a switch through the caches equals one through fresh objects.
     TEST("KsCache.KeyCache.core", [] {

@@ -173,3 +173,18 @@ def test_configs3_line_at_eight_ranks():
     assert c["workload"].startswith("configs[3]") and "tower-sharded x8" in c["parallelism"]
     c = bench.headline_config("batch", 8, 16, 16, 1024)
     assert c["global_batch"] == 8 * 1024 and c["batch_per_gpu"] == 1024
+
+
+def test_eight_rank_launch_reports_every_rank():
+    """The driver's 8-GPU launch shape rehearsed on the CPU (gloo): --gpus 8
+    starts eight ranks, each joins the group, the key broadcaster agrees on
+    one backend across all of them and the line names all eight ranks'
+    communicator outcomes."""
+    r = subprocess.run([sys.executable, BENCH, "--gpus", "8", "--launch-check"], capture_output=True, text=True,
+                       timeout=600, env=_env())
+    assert r.returncode == 0, r.stderr[-2000:]
+    out = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
+    assert out["n_gpus"] == 8 and sorted(out["ranks"]) == list(range(8)) and len(set(out["pids"])) == 8
+    assert sorted(x["rank"] for x in out["evalkey_broadcast"]["ranks"]) == list(range(8))
+    assert out["evalkey_broadcast"]["verified"] is True
+    assert out["evalkey_broadcast_capi"]["per_rank"]["launch_check"]["comm_failed"] == list(range(8))
