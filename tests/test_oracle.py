@@ -20,6 +20,37 @@ def test_kat_transform(O):
     assert O.ntt_inv(AB, tb).reshape(-1).tolist() == k["expected"]
 
 
+def test_forward_is_evaluation_at_odd_powers(O):
+    """The identity tests/test_gpu_definition.py checks the GPU against at
+    full size: the forward transform leaves a(psi^(2 rev(i) + 1)) at slot i.
+    On the reference's own KAT (UnitTestTransform.cpp:60-94, N = 4, q = 113)
+    and on the oracle at N = 2^5 .. 2^10 (the oracle pinned by that KAT), with
+    exact Python integers."""
+    import random
+
+    def rev(x, bits):
+        return int(format(x, f"0{bits}b")[::-1], 2) if bits else 0
+
+    def evaluate(a, x, q):
+        v = 0
+        for c in reversed(a):
+            v = (v * x + c) % q
+        return v
+
+    k = REF["kat_transform"]
+    q, psi, n = k["q"], k["root"], k["m"] // 2
+    A = O.ntt_fwd(O.U(k["a"]).reshape(1, 1, -1), O.Tables(n, [q], [psi])).reshape(-1)
+    assert [evaluate(k["a"], pow(psi, 2 * rev(i, 2) + 1, q), q) for i in range(n)] == [int(v) for v in A]
+    rng = random.Random(3)
+    for log_n in (5, 7, 10):
+        n = 1 << log_n
+        qs, rs = O.moduli_chain(log_n, 1)
+        a = [rng.randrange(qs[0]) for _ in range(n)]
+        y = O.ntt_fwd(O.U(a).reshape(1, 1, -1), O.Tables(n, qs, rs)).reshape(-1)
+        for i in range(0, n, max(1, n // 64)):
+            assert int(y[i]) == evaluate(a, pow(rs[0], 2 * rev(i, log_n) + 1, qs[0]), qs[0])
+
+
 def test_kat_mubintvec(O):
     """UnitTestMubintvec.cpp:276-359 basic_vector_vector_mod_math_1_limb."""
     k = REF["kat_mubintvec"]
