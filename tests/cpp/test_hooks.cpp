@@ -13,6 +13,7 @@
 #include <cstdio>
 #include <random>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "mock_openfhe.hpp"
@@ -330,6 +331,40 @@ static void keyswitch(FILE* dump) {
     ofhe::hooks::EraseEvalKey("relin");
 }
 
+// DCRTPoly operators are called from OpenMP worker threads (SURVEY.md
+// §8(b), dcrtpoly.h:144,175,196): four threads run the device hooks at once
+// on their own polynomials (thread-local pinned staging, one shared context,
+// plan and converter caches behind their locks) and each result must equal
+// the oracle's.
+static void concurrent_hooks() {
+    const uint32_t log_n = 13, n = 1u << log_n, T = 6;
+    std::vector<uint64_t> q(T), r(T);
+    oracle_moduli_chain(60, 2 * n, T, q.data(), r.data());
+    const int threads = 4, reps = 6;
+    std::vector<int> bad(threads, 0);
+    std::vector<std::thread> pool;
+    for (int w = 0; w < threads; w++)
+        pool.emplace_back([&, w] {
+            std::mt19937_64 rng(1000 + w);
+            for (int k = 0; k < reps; k++) {
+                auto a = mock::make_towers(n, q, r, rng), b = mock::make_towers(n, q, r, rng, Format::EVALUATION);
+                mock::DCRTPolyImpl d{Format::COEFFICIENT, a}, e{Format::EVALUATION, b};
+                d.SwitchFormat();  // forward on the device
+                d *= e;            // the gate is forced to the device: TimesEq too
+                for (uint32_t t = 0; t < T; t++) {
+                    auto want = ntt(words(a[t]), q[t], r[t], true);
+                    auto wb = words(b[t]);
+                    oracle_vec_modmul(want.data(), wb.data(), want.data(), n, q[t]);
+                    bad[w] += words(d.m_vectors[t]) != want;
+                }
+            }
+        });
+    for (auto& th : pool) th.join();
+    int total = 0;
+    for (int v : bad) total += v;
+    CHECK(total == 0, "four threads' concurrent SwitchFormat + *= hooks equal the oracle");
+}
+
 int main(int argc, char** argv) {
     FILE* dump = argc > 1 ? std::fopen(argv[1], "wb") : nullptr;
     try {
@@ -338,6 +373,9 @@ int main(int argc, char** argv) {
             ofhe::hooks::set_policy(ofhe::hooks::Policy::all(device ? ofhe::hooks::kAlways : ofhe::hooks::kNever));
             element_hooks(12, device);
         }
+        g_mode = "threads";
+        ofhe::hooks::set_policy(ofhe::hooks::Policy::all(ofhe::hooks::kAlways));
+        concurrent_hooks();
         g_mode = "keyswitch";
         keyswitch(dump);
         // the measured gate: what Policy::measured() says for a few shapes, and
