@@ -144,3 +144,40 @@ def test_pipeline_is_pointwise_product_at_configs2_ring(hip):
         for i in _samples(n, 41 + t, k=4):
             xi = pow(psi, 2 * _rev(i, log_n) + 1, q)
             assert _evaluate(co, xi, q) == _evaluate(ao, xi, q) * int(b[0, t, i]) % q, (t, i)
+
+
+@pytest.mark.parametrize("sq,sp", [(48, 16), (16, 48)])
+def test_base_conversion_is_crt_sum_full_size(hip, sq, sp):
+    """ApproxSwitchCRTBasis (dcrtpoly-impl.h:1034-1063) at configs[4]'s ring,
+    N = 2^17: Q = 48 -> P = 16 (ModDown's direction, sizes swapped) and a
+    16-tower digit -> 48 towers (ModUp's), on sampled coefficients against its
+    definition with exact integers: out_j = (sum_i [x_i (Q/q_i)^-1]_{q_i} *
+    (Q/q_i)) mod p_j -- one big-integer sum per coefficient, reduced once,
+    against the kernel's per-term residues, 128-bit sums and Barrett
+    reduction (matrix cores on this shape)."""
+    import torch
+
+    H, ctx = hip
+    import bench
+
+    log_n = 17
+    n = 1 << log_n
+    chain, _ = bench.moduli_chain(log_n, sq + sp)
+    q, p = chain[:sq], chain[sq:]
+    Q = 1
+    for qi in q:
+        Q *= qi
+    qhat = [Q // qi for qi in q]
+    qhinv = [pow(h % qi, -1, qi) for h, qi in zip(qhat, q)]
+    qhmodp = [h % pj for h in qhat for pj in p]
+    rng = np.random.default_rng(sq)
+    x = np.stack([rng.integers(0, qi, size=n, dtype=np.uint64) for qi in q])[None]
+    bc = H.BaseConverter(ctx, log_n, q, p, qhinv, qhmodp)
+    out = torch.empty((1, sp, n), dtype=torch.int64, device="cuda")
+    dx = _dev(x)
+    bc.switch(dx.data_ptr(), out.data_ptr(), 1, _stream())
+    got = _host(out)
+    bc.close()
+    for c in _samples(n, 5 + sq, k=24):
+        s = sum(int(x[0, i, c]) * qhinv[i] % q[i] * qhat[i] for i in range(sq))
+        assert [int(got[0, j, c]) for j in range(sp)] == [s % pj for pj in p], c
