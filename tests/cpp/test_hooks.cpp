@@ -327,6 +327,16 @@ static void keyswitch(FILE* dump) {
             thrown = true;
         }
         CHECK(thrown, "KeySwitchCore without a resident key throws math_error");
+        thrown = false;
+        try {
+            Towers coeff = ks.bv[0];
+            coeff[1].OverrideFormat(Format::COEFFICIENT);
+            std::vector<const Towers*> one{&coeff};
+            ofhe::hooks::PutEvalKey("bad", one, one, sp);
+        } catch (const ofhe::math_error&) {
+            thrown = true;
+        }
+        CHECK(thrown, "PutEvalKey with a coefficient-form key tower throws math_error");
     }
     ofhe::hooks::EraseEvalKey("relin");
 }

@@ -529,7 +529,11 @@ void PutEvalKey(const std::string& tag, const std::vector<const Towers*>& bv, co
     fa.reserve(dnum * T * n);
     for (size_t j = 0; j < dnum; j++) {
         for (int which = 0; which < 2; which++) {
-            TowerView vj = view(const_cast<Towers&>(*(which ? av[j] : bv[j])));
+            const Towers& tj = *(which ? av[j] : bv[j]);
+            using Fmt = std::decay_t<decltype(tj[0].GetFormat())>;
+            for (const auto& tw : tj)
+                if (tw.GetFormat() != Fmt::EVALUATION) throw math_error("hooks::PutEvalKey: EVALUATION form expected");
+            TowerView vj = view(const_cast<Towers&>(tj));
             if (vj.q != v0.q || vj.psi != v0.psi || vj.n != v0.n)
                 throw math_error("hooks::PutEvalKey: key polynomials over different bases");
             auto& f = which ? fa : fb;
