@@ -86,6 +86,10 @@ def test_argument_errors_without_device():
         L.ofhe_hip_comm_init(null, 2, 0, null, ctypes.byref(vp())),
         L.ofhe_hip_comm_destroy(null),
         L.ofhe_hip_bcast_evalkey(null, null, 8, 0, null),
+        L.ofhe_hip_event_create(null, ctypes.byref(vp())),
+        L.ofhe_hip_event_record(null, null),
+        L.ofhe_hip_event_sync(null),
+        L.ofhe_hip_event_destroy(null),
     ]
     assert all(rc != 0 for rc in cases), cases
     assert L.ofhe_hip_last_error()  # a message is set

@@ -72,3 +72,30 @@ def test_free_async_refuses_foreign_and_double_frees():
     ctx.free_async(q, s)
     ctx.sync(s)
     ctx.close()
+
+
+def test_event_marks_stream_work_and_outlives_its_context():
+    """ofhe_hip_event_* (the adapter's staged-copy ordering): an event recorded
+    after a copy on the stream, synchronised, sees the copy done; an event made
+    before ofhe_hip_finalize is still destroyed cleanly after it (it keeps the
+    device id, not the freed context)."""
+    import ctypes
+
+    import torch
+
+    import ofhe_hip as H
+
+    L = H.lib()
+    vp = ctypes.c_void_p
+    ctx = H.Context(0)
+    s = stream()
+    ev = vp()
+    H._check(L.ofhe_hip_event_create(ctx.handle, ctypes.byref(ev)))
+    src = torch.arange(1 << 20, dtype=torch.int64, device="cuda")
+    dst = torch.empty_like(src)
+    ctx.copy_device(dst.data_ptr(), src.data_ptr(), src.numel() * 8, s)
+    H._check(L.ofhe_hip_event_record(ev, vp(s or None)))
+    H._check(L.ofhe_hip_event_sync(ev))
+    assert torch.equal(dst, src)
+    ctx.close()  # frees the context
+    H._check(L.ofhe_hip_event_destroy(ev))

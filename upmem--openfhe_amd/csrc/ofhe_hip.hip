@@ -201,17 +201,20 @@ int ofhe_hip_sync(ofhe_ctx_t ctx, void* stream) {
 // A completion marker on one stream: waiting on it waits for that stream's
 // work up to the record, nothing queued after it (the adapter's staging
 // buffers are reused once their DMA has read them, ofhe_dcrt.hpp).
+// It keeps the device id, not the context: an event may outlive the context
+// that made it (ofhe_hip_finalize frees the context).
 struct ofhe_event_s {
-    ofhe_ctx_t ctx = nullptr;
+    int device = 0;
     hipEvent_t ev = nullptr;
 };
 
 int ofhe_hip_event_create(ofhe_ctx_t ctx, ofhe_event_t* out) {
     if (!ctx || !out) return fail(OFHE_ERR_ARG, "NULL argument");
+    if (ctx->live.load() == 0) return fail(OFHE_ERR_STATE, "context finalized");
     HIPCHK(hipSetDevice(ctx->device));
     hipEvent_t e = nullptr;
     HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-    *out = new ofhe_event_s{ctx, e};
+    *out = new ofhe_event_s{ctx->device, e};
     return OFHE_OK;
 }
 
@@ -229,7 +232,7 @@ int ofhe_hip_event_sync(ofhe_event_t ev) {
 
 int ofhe_hip_event_destroy(ofhe_event_t ev) {
     if (!ev) return fail(OFHE_ERR_ARG, "event is NULL");
-    (void)hipSetDevice(ev->ctx->device);
+    (void)hipSetDevice(ev->device);
     (void)hipEventDestroy(ev->ev);
     delete ev;
     return OFHE_OK;
