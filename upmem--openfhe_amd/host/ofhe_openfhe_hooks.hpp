@@ -97,12 +97,15 @@ inline Staging& staging(int device, size_t words, int slot = 0) {
 
 // ---------------------------------------------------------------------------
 // The gate.  HookOp names a hook; the device takes a call when the ring
-// dimension n >= 2^min_log_n[op][tower class].  Tower classes are the tower
-// counts the crossover was measured at: T < 8 (T = 1), 8 <= T < 16, 16 <= T <
-// 48, T >= 48.  kNever keeps an op on the CPU loop at every measured size (the
-// element-wise hooks: at 24 PCIe bytes per coefficient the host-buffer path
-// cannot beat a host loop that streams the same words from DRAM; they pay
-// only in the resident integration, DCRTPolyHip).  Rings below kDeviceMinRing
+// dimension n >= 2^min_log_n[op][tower class].  Tower classes bracket the
+// tower counts the crossover was measured at, T = 1, 8, 16, 48 Q towers:
+// T < 8, 8 <= T < 16, 16 <= T < 48, T >= 48, counted as the hook sees them
+// (the basis ops and the key switch count Q + P with P = ceil(Q / 3), which
+// falls in the same class as Q for every measured point).  kNever keeps an op
+// on the CPU loop at every measured size (the element-wise hooks: at 16-24
+// PCIe bytes per coefficient the host-buffer path cannot beat a host loop
+// over the same words in the host's memory and caches; they pay only in the
+// resident integration, DCRTPolyHip).  Rings below kDeviceMinRing
 // (binfhe's, N <= 2^11, rgsw-acc-*.cpp) always stay on the CPU.
 // ---------------------------------------------------------------------------
 enum class HookOp : int {
