@@ -188,3 +188,39 @@ def test_eight_rank_launch_reports_every_rank():
     assert sorted(x["rank"] for x in out["evalkey_broadcast"]["ranks"]) == list(range(8))
     assert out["evalkey_broadcast"]["verified"] is True
     assert out["evalkey_broadcast_capi"]["per_rank"]["launch_check"]["comm_failed"] == list(range(8))
+
+
+def test_keyswitch_roofline_counts():
+    """configs[4]'s key-switch bound (bench.keyswitch_roofline): 320 transforms
+    per key switch at Q = 48, P = 16, dnum = 3 (ModUp: 3 digits x (16 INTT +
+    48 NTT); each ModDown: 16 INTT + 48 NTT) and the inner product's 3.09 GB at
+    batch 8 (keyswitch-hybrid.cpp:330-482)."""
+    import bench
+
+    n = 1 << 17
+    r = bench.keyswitch_roofline(48, 16, 3, n, 8, 3.35, {"inner_product": 0.53}, 1.44e11, 1.40e11)
+    assert r["transforms_per_keyswitch"] == {"ntt": 240, "intt": 80, "total": 320}
+    assert r["inner_product"]["alg_bytes"] == 8 * n * 64 * (8 * 3 + 2 * 3 + 2 * 8) == 3087007744
+    want = 8 * n * (240 / 1.44e11 + 80 / 1.40e11) * 1e3 + 3087007744 / 8e12 * 1e3
+    assert abs(r["bound_ms"] - want) < 1e-9 and abs(r["frac"] - want / 3.35) < 1e-12
+    # a lower level: l = 40 towers -> digits of 16, 16, 8
+    r = bench.keyswitch_roofline(40, 16, 3, n, 1, 1.0, {}, 1e11, 1e11)
+    assert r["transforms_per_keyswitch"]["intt"] == 40 + 32
+    assert r["transforms_per_keyswitch"]["ntt"] == (40 - 14 + 16) * 0 + sum(40 - c + 16 for c in (14, 14, 12)) + 80
+
+
+def test_hook_gate_matches_the_committed_crossover():
+    """Policy::measured() in host/ofhe_openfhe_hooks.hpp is the table that
+    tests/cpp/hook_crossover.cpp printed on the MI355X box
+    (profiles/r06_hook_crossover.txt)."""
+    import re
+
+    from conftest import ROOT
+
+    prof = open(os.path.join(ROOT, "profiles", "r06_hook_crossover.txt")).read()
+    hdr = open(os.path.join(ROOT, "upmem--openfhe_amd", "host", "ofhe_openfhe_hooks.hpp")).read()
+    pat = re.compile(r"/\*\s*(\w+)\s*\*/\s*\{([^}]*)\}")
+    measured = dict((m.group(1), m.group(2).replace(" ", "")) for m in pat.finditer(prof.split("# Policy::measured()")[1]))
+    body = hdr.split("static Policy measured()")[1].split("for (int o = 0;")[0]
+    shipped = dict((m.group(1), m.group(2).replace(" ", "")) for m in pat.finditer(body))
+    assert len(measured) == 10 and measured == shipped
