@@ -139,18 +139,22 @@ struct Policy {
     // measured: tests/cpp/hook_crossover.cpp on the MI355X box (host
     // buffers, pipelined pinned staging, both PCIe directions; the CPU loop
     // on 16 OpenMP threads), device taken where it wins by >= 10 % at that
-    // N and every larger one (profiles/r06_hook_crossover.txt)
+    // N and every larger one; two runs on two boxes
+    // (profiles/r06_hook_crossover.txt, r06m_hook_crossover.txt), entry by
+    // entry the larger (the CPU kept where either run put the crossover
+    // higher; the runs differ by one step at four borderline entries).
+    // DESIGN.md (b).
     static Policy measured() {
         Policy p{};
         const uint8_t table[kHookOps][4] = {
-            /* SwitchFormat          */ {13, 13, 14, 13},
+            /* SwitchFormat          */ {13, 14, 14, 13},
             /* TimesEq               */ {16, kNever, kNever, kNever},
             /* PlusEq                */ {kNever, kNever, kNever, kNever},
             /* MinusEq               */ {kNever, kNever, kNever, kNever},
-            /* ApproxSwitchCRTBasis  */ {17, 13, 12, 12},
+            /* ApproxSwitchCRTBasis  */ {17, 14, 12, 12},
             /* ApproxModUp           */ {14, 12, 12, 12},
             /* ApproxModDown         */ {12, 12, 12, 12},
-            /* AutomorphismTransform */ {13, 13, 14, 14},
+            /* AutomorphismTransform */ {13, 14, 14, 14},
             /* ScalarEq              */ {kNever, kNever, kNever, kNever},
             /* KeySwitchCore         */ {12, 12, 12, 12},
         };
