@@ -1034,7 +1034,7 @@ def host_cpu():
     cap = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or avail
     # one thread per physical core among the CPUs this process may use, within OMP_NUM_THREADS
     cores = max(1, min(cap, avail // max(1, tpc), phys))
-    return cores, model, phys, tpc
+    return cores, model, phys, tpc, avail
 
 
 def cpu_baseline(args, qs, roots, log_n, T):
@@ -1042,7 +1042,7 @@ def cpu_baseline(args, qs, roots, log_n, T):
     import oracle as O
 
     n = 1 << log_n
-    cores, model, phys, tpc = host_cpu()
+    cores, model, phys, tpc, avail = host_cpu()
     tbs = O.Tables(n, qs, roots)
     # single thread, one polynomial of all towers (the reference's 41.1 ms figure)
     O.lib().oracle_set_threads(1)
@@ -1070,6 +1070,9 @@ def cpu_baseline(args, qs, roots, log_n, T):
             "sample": f"{runs} runs x {Bs} polys x {T} towers x N=2^{log_n} ({el:.1f} s), "
                       f"oracle/ofhe_oracle.c, OpenMP over batch x towers on {cores} threads",
             "cpu_model": model, "physical_cores_reported": phys, "threads_per_core": tpc,
+            "threads_note": f"{cores} threads: one per physical core of the {avail} logical CPUs in this "
+                            f"process's affinity ({tpc} per core), within OMP_NUM_THREADS "
+                            f"{os.environ.get('OMP_NUM_THREADS', 'unset')}; the host has {phys} physical cores",
             "host": socket.gethostname(),
             "single_thread_ms_per_poly": one_ms, "single_thread_coeffs_per_s": T * n / (one_ms * 1e-3),
             "reference_single_thread_ms_per_poly": REF_CPU_MS_1T,
