@@ -86,7 +86,7 @@ inline std::vector<const uint64_t*> cptr(const std::vector<uint64_t*>& p) {
 // One pool per (thread, device), slots grow to the largest size asked for;
 // every hook ends with a synchronous download, so a slot is idle when reused.
 // Cost: each calling thread keeps two pinned slots (plus their device
-// twins) as large as its largest hooked call -- 2 x 50 MiB for a key switch at
+// twins) as large as its largest hooked call -- 48 + 96 MiB for a key switch at
 // N = 2^17, 48 towers -- until the thread exits.
 inline Staging& staging(int device, size_t words, int slot = 0) {
     thread_local std::map<std::pair<int, int>, std::unique_ptr<Staging>> pool;
